@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- CSR SpMV effective HBM GB/s on MI355X (BASELINE.json metric).
+
+Default (N=1): BASELINE config 2 -- B is 2^20 x 2^20 with exactly 16 distinct
+uniformly random columns per row (fp32 values from a 255-entry codebook),
+y = B x + 0.5 y with the stream kernel.  A step is one SpMV over one matrix.
+To measure HBM rather than the 256 MiB Infinity Cache, steps rotate over
+`--replicas` independent copies (matrix, x, y): 4 x 151 MB per rank.
+
+N>1 (torchrun, one process per GPU): weak scaling -- every rank owns 2^20 rows
+of a (N*2^20) x (N*2^20) matrix with global columns; a step is one RCCL
+all-gather of x (xGMI) followed by the local SpMV.  `value` is the sum of all
+ranks' algorithmic bytes divided by the max-over-ranks step time.
+
+Algorithmic bytes per SpMV: 8*nnz + 4*(rows+1) + 4*cols + 8*rows.
+
+Also reported, on the same JSON line:
+  roofline      the SpMV kernel alone: algorithmic bytes / mean kernel time
+                (HIP events around each launch on the launch stream) vs 8 TB/s;
+                `traffic` from rocprofv3 PMC (profiles/) when available.
+  cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C, 1 thread)
+                on the same matrix, ~10 s of CPU work.
+  spmm          config 3 (same matrix, N=32 right-hand sides), GFLOP/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def spmv_bytes(nnz: int, rows: int, cols: int) -> int:
+    return 8 * nnz + 4 * (rows + 1) + 4 * cols + 8 * rows
+
+
+def spmm_bytes(nnz: int, rows: int, cols: int, n: int) -> int:
+    return 8 * nnz + 4 * (rows + 1) + 4 * n * cols + 8 * n * rows
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch measured by rocprofv3 PMC (tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--per-row", type=int, default=16)
+    ap.add_argument("--replicas", type=int, default=4)
+    ap.add_argument("--algo", default="stream")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-spmm", action="store_true")
+    ap.add_argument("--spmm-n", type=int, default=32)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import sparsematrix_amd as smd
+    from sparsematrix_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (use torch.distributed.run)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    smd.load()
+
+    R = args.rows_per_rank
+    C = R * world                          # global columns (= global rows)
+    per = args.per_row
+    reps = []
+    for k in range(args.replicas):
+        seed = 2 + 1000 * k + 7919 * rank
+        rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
+        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=local_rank)
+        g = torch.Generator(device=dev).manual_seed(seed + 1)
+        x_local = torch.rand(R, generator=g, device=dev) * 2 - 1
+        x_full = torch.empty(C, device=dev) if world > 1 else x_local
+        y = torch.rand(R, generator=g, device=dev) * 2 - 1
+        reps.append(dict(M=M, rp=rp, ci=ci, va=va, x_local=x_local, x_full=x_full, y=y))
+        if k:
+            del rp, ci, va
+    nnz = R * per
+    bytes_rank = spmv_bytes(nnz, R, C)
+    torch.cuda.synchronize()
+
+    def step(i, ev=None):
+        r = reps[i % len(reps)]
+        if world > 1:
+            dist.all_gather_into_tensor(r["x_full"], r["x_local"])
+        if ev is not None:
+            ev[0].record()
+        r["M"].spmv(r["x_full"], r["y"], 1.0, 0.5, algo=args.algo)
+        if ev is not None:
+            ev[1].record()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = bytes_rank * world / (elapsed / args.steps) / 1e9
+    kmean = float(np.mean(kern_ms))
+    kmed = float(np.median(kern_ms))
+    achieved = bytes_rank / (kmean * 1e-3) / 1e9
+    workload = f"spmv_{R}x{C}_{per}_per_row"
+    traffic = load_traffic(workload) if world == 1 else None
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+            "traffic": traffic, "kernel": "spmv_stream_kernel",
+            "kernel_ms_mean": round(kmean, 5), "kernel_ms_median": round(kmed, 5),
+            "alg_bytes_per_launch": bytes_rank}
+
+    # ---- SpMM (config 3) on replica 0, same ranks ---------------------------------
+    spmm = None
+    if not args.no_spmm:
+        N = args.spmm_n
+        r0 = reps[0]
+        g = torch.Generator(device=dev).manual_seed(3)
+        X = torch.rand((C, N), generator=g, device=dev) * 2 - 1
+        Y = torch.rand((R, N), generator=g, device=dev) * 2 - 1
+        for _ in range(3):
+            r0["M"].spmm(X, Y, 1.0, 0.5)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(10)]
+        for a, b in ev:
+            a.record()
+            r0["M"].spmm(X, Y, 1.0, 0.5)
+            b.record()
+        torch.cuda.synchronize()
+        sm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        sb = spmm_bytes(nnz, R, C, N)
+        spmm = {"n_rhs": N, "ms": round(sm_ms, 4),
+                "gflops": round(2.0 * nnz * N / (sm_ms * 1e-3) / 1e9, 1),
+                "hbm_gbs": round(sb / (sm_ms * 1e-3) / 1e9, 1),
+                "hbm_frac": round(sb / (sm_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                "kernel": "spmm_rowpanel_kernel<8>", "mfma": "not used (fp32 SpMM at "
+                "~2 flop/B is HBM/gather bound; see DESIGN.md)"}
+        del X, Y
+
+    # ---- CPU baseline (rank 0, N = 1) --------------------------------------------
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu:
+        import oracle
+        r0 = reps[0]
+        rp = r0["rp"].cpu().numpy()
+        ci = r0["ci"].cpu().numpy()
+        va = r0["va"].cpu().numpy()
+        x = r0["x_full"].cpu().numpy()
+        y0 = r0["y"].cpu().numpy()
+        oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)          # warm
+        n_rep, t_cpu = 0, 0.0
+        while t_cpu < args.cpu_seconds and n_rep < 200:
+            c0 = time.perf_counter()
+            oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)
+            t_cpu += time.perf_counter() - c0
+            n_rep += 1
+        cpu = {"value": round(bytes_rank * n_rep / t_cpu / 1e9, 3), "unit": "GB/s", "cores": 1,
+               "kind": "port",
+               "sample": f"oracle same-order CSR SpMV (C, 1 thread) on the full config-2 matrix "
+                         f"(replica 0), {n_rep} reps in {t_cpu:.1f} s",
+               "ms_per_spmv": round(1e3 * t_cpu / n_rep, 3), "cpu": cpu_model(),
+               "nproc": os.cpu_count()}
+
+    if rank == 0:
+        line = {
+            "metric": "CSR SpMV effective HBM GB/s", "value": round(value, 1), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": workload, "rows_per_rank": R, "cols": C, "nnz_per_rank": nnz,
+                       "per_row": per, "replicas": args.replicas, "algo": args.algo,
+                       "alpha": 1.0, "beta": 0.5,
+                       "parallelism": f"row-partition x{world}" + (", RCCL all-gather(x)"
+                                                                   if world > 1 else "")},
+            "roofline": roof, "cpu_baseline": cpu, "spmm": spmm,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

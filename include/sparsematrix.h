@@ -1,0 +1,195 @@
+/*
+ * sparsematrix.h -- C ABI of sparsematrix_amd (libsparsematrix_amd.so), an
+ * MI355X-native (gfx950) replacement for NeverLEX/sparsematrix's sparse x dense
+ * multiply.  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * Orientation.  The reference stores S (k x n) and computes, for a dense
+ * row-major A (m x k) and C (m x n),  C = alpha*A*S + beta*C
+ * (sparse-matrix.h:37, sparse-matrix.cc:139-194).  Here the matrix is held on
+ * the device as CSR of B = S^T (n rows x k columns, int32 row_ptr/col_idx,
+ * fp32 values), so m = 1 is the SpMV  y = alpha*B*x + beta*y  and a panel of
+ * N right-hand sides is the SpMM  Y = alpha*B*X + beta*Y  (X: k x N, Y: n x N,
+ * both row-major).  sm_num_rows/sm_num_cols report the reference's S view
+ * (rows_ = k, cols_ = n; sparse-matrix.h:39-40).
+ *
+ * Semantics kept from the reference (SURVEY.md §7 "Drop-in semantics"):
+ *   - beta is applied by multiplication whenever beta != 1 (so beta = 0
+ *     propagates NaN/Inf already in C/y)                 kernel.cc:10-29
+ *   - alpha == 0 skips the product entirely              sparse-matrix.cc:152
+ *   - alpha is folded into the stored value first: each term is
+ *     x * (v * alpha), added one at a time               kernel.cc:791, 580-582
+ *   - ids >= table_size are not stored; explicit 0.0 table entries are
+ *                                                        sparse-matrix.cc:44, 77
+ * Summation order: SM_ALGO_PARITY adds the terms of every output in stored
+ * (ascending column) order, exactly as the reference does, so results are
+ * bit-identical to the reference CPU kernel.  SM_ALGO_AUTO/STREAM/SPMM keep
+ * that order for rows of up to SM_SERIAL_ROW_MAX terms and use a tree sum for
+ * longer rows; the bound for those is |y - y_ref| <= 1e-6 * sum|terms|.
+ *
+ * Errors: every call returns sm_status; sm_last_error() gives a message for
+ * the calling thread.  Device calls are asynchronous on `stream` (a
+ * hipStream_t; NULL = the legacy default stream) unless stated otherwise.
+ */
+#ifndef SPARSEMATRIX_AMD_H
+#define SPARSEMATRIX_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define SM_API __attribute__((visibility("default")))
+#else
+#define SM_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum sm_status {
+    SM_OK = 0,
+    SM_ERR_INVALID_ARG = 1,     /* bad shape, stride, pointer or enum          */
+    SM_ERR_OUT_OF_MEMORY = 2,   /* host or device allocation failed            */
+    SM_ERR_HIP = 3,             /* a HIP runtime call failed                   */
+    SM_ERR_NOT_SUPPORTED = 4,   /* operation not available for this matrix     */
+    SM_ERR_TOO_LARGE = 5,       /* exceeds int32 indexing (nnz or rows >= 2^31) */
+    SM_ERR_INVALID_MATRIX = 6,  /* CSR failed validation (col out of range...) */
+    SM_ERR_NO_DEVICE = 7        /* no HIP device visible                       */
+} sm_status;
+
+/* SBLAS_TRANSPOSE, sparse-matrix.h:20-23 */
+typedef enum sm_trans { SM_NO_TRANS = 0, SM_TRANS = 1 } sm_trans;
+
+typedef enum sm_algo {
+    SM_ALGO_AUTO = 0,     /* stream (SpMV) / row-panel (SpMM) kernels              */
+    SM_ALGO_PARITY = 1,   /* bit-exact with the reference for every row            */
+    SM_ALGO_STREAM = 2,   /* nnz-balanced row tiles through LDS (+ long-row split) */
+    SM_ALGO_VECTOR = 3    /* one wavefront per row, DPP/shuffle reduction          */
+} sm_algo;
+
+/* Rows with at most this many terms are summed in reference order by the
+ * fast kernels (bit-exact); longer rows use a tree reduction. */
+#define SM_SERIAL_ROW_MAX 64
+
+typedef struct sm_matrix sm_matrix;   /* opaque, device-resident */
+typedef void *sm_stream;              /* hipStream_t */
+
+typedef struct sm_info {
+    int64_t s_rows, s_cols;     /* reference S view: rows_ = k, cols_ = n      */
+    int64_t n_rows, n_cols;     /* CSR of B = S^T: n rows, k columns          */
+    int64_t nnz;                /* stored entries (explicit zeros included)    */
+    int32_t table_size;         /* codebook size T (0 if built from CSR)       */
+    int32_t has_ref_stream;     /* 1 if the reference encoding is held         */
+    int64_t n_entries;          /* reference stream length (nnz + fillers)     */
+    int64_t n_panels;           /* reference panels (block_bounds_.size())     */
+    int32_t device;             /* HIP device ordinal holding the matrix       */
+    int32_t n_tiles;            /* stream-kernel row tiles                     */
+    int32_t n_long_rows;        /* rows split across workgroups                */
+    int32_t max_row_nnz;        /* longest row                                 */
+    int64_t device_bytes;       /* device memory held by the matrix            */
+} sm_info;
+
+/* ---- library ----------------------------------------------------------- */
+SM_API const char *sm_version(void);
+SM_API const char *sm_status_string(sm_status s);
+SM_API const char *sm_last_error(void);
+SM_API sm_status sm_device_count(int32_t *count);
+
+/* ---- construction ---------------------------------------------------------
+ * sm_create_from_dense_index: replaces SparseMatrix::CopyForm
+ * (sparse-matrix.cc:20-99; ctor sparse-matrix.h:29-31).  `index` is a
+ * rows x stride uint8 matrix of codebook ids; ids >= table_size are empty.
+ * NoTrans: S = index (rows x cols).  Trans: S = index^T (cols x rows).
+ * table_size must be in [0, 255]; 0 yields an empty 0 x 0 matrix
+ * (sparse-matrix.cc:25-26).  Host pointers; the CSR is uploaded to `device`. */
+SM_API sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t cols,
+                                            int32_t stride, const float *table,
+                                            int32_t table_size, sm_trans trans,
+                                            int32_t device, sm_matrix **out);
+
+/* Additive CSR ingestion (no reference equivalent: the reference cannot encode
+ * the north-star sizes).  B is n_rows x n_cols; row_ptr has
+ * n_rows+1 entries.  Host pointers, validated on the host. */
+SM_API sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                    const int32_t *row_ptr, const int32_t *col_idx,
+                                    const float *val, int32_t device, sm_matrix **out);
+
+/* Same, from device pointers on `device` (copied device-to-device on `stream`
+ * and validated by a kernel; synchronises `stream`). */
+SM_API sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                           const int32_t *d_row_ptr, const int32_t *d_col_idx,
+                                           const float *d_val, int32_t device, sm_stream stream,
+                                           sm_matrix **out);
+
+/* Destroy: sparse-matrix.cc:9-18 (frees host and device storage). */
+SM_API void sm_destroy(sm_matrix *m);
+
+/* ---- queries ----------------------------------------------------------- */
+SM_API sm_status sm_get_info(const sm_matrix *m, sm_info *info);
+SM_API int32_t sm_num_rows(const sm_matrix *m);   /* NumRows, sparse-matrix.h:39 */
+SM_API int32_t sm_num_cols(const sm_matrix *m);   /* NumCols, sparse-matrix.h:40 */
+
+/* The reference encoding (sparse-matrix.h:46-52): E delta steps and ids, and
+ * per panel (row_off, col_off, begin, end).  Sizes from sm_get_info. */
+SM_API sm_status sm_copy_ref_stream(const sm_matrix *m, uint8_t *pos, uint8_t *val,
+                                    int32_t *panel_row_off, int32_t *panel_col_off,
+                                    int64_t *panel_begin, int64_t *panel_end);
+
+/* Host copy of the device CSR (row_ptr n_rows+1, col_idx/val nnz). */
+SM_API sm_status sm_copy_csr(const sm_matrix *m, int32_t *row_ptr, int32_t *col_idx, float *val);
+
+/* CopyTo (sparse-matrix.cc:101-137), host output.  NoTrans writes S
+ * (s_rows x stride), Trans writes S^T (s_cols x stride); untouched elements
+ * are zeroed.  Decoded on the device. */
+SM_API sm_status sm_to_dense(const sm_matrix *m, float *out, int32_t stride, sm_trans trans);
+
+/* operator== (sparse-matrix.cc:197-207) on semantic content: shape, stored
+ * (row, col, value) triples and, for codebook matrices, the table. */
+SM_API int32_t sm_equal(const sm_matrix *a, const sm_matrix *b);
+
+/* ---- compute on device pointers ----------------------------------------- */
+/* y[n_rows] = alpha * B * x[n_cols] + beta * y */
+SM_API sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, float *y,
+                         sm_algo algo, sm_stream stream);
+
+/* Y (n_rows x n_rhs, ldy) = alpha * B * X (n_cols x n_rhs, ldx) + beta * Y */
+SM_API sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X,
+                         int64_t ldx, float beta, float *Y, int64_t ldy, sm_algo algo,
+                         sm_stream stream);
+
+/* AddMatMat (sparse-matrix.cc:139-194) on device pointers:
+ * C (m x n, ldc) = alpha * A (m x k, lda) * S + beta * C. */
+SM_API sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
+                              float *c, int32_t ldc, float alpha, float beta, sm_algo algo,
+                              sm_stream stream);
+
+/* Synchronous drop-in for AddMatMat on HOST pointers (uploads A and C,
+ * computes with SM_ALGO_PARITY, downloads C).  Bit-identical to the reference. */
+SM_API sm_status sm_addmatmat_host(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
+                                   float *c, int32_t ldc, float alpha, float beta);
+
+/* ---- kernel.h helpers (kernel.cc:10-187), device pointers ---------------- */
+/* c[i*ldc + j] *= beta for i < m, j < n */
+SM_API sm_status sm_beta_scale(float *c, int32_t m, int32_t n, int32_t ldc, float beta,
+                               sm_stream stream);
+/* sa[j*ldsa + i] = a[i*lda + j] for i < m, j < n (out of place) */
+SM_API sm_status sm_transpose(const float *a, int32_t m, int32_t n, int32_t lda, float *sa,
+                              int32_t ldsa, sm_stream stream);
+
+/* ---- reference-format panel kernels (kernel.h:42-62), device pointers -----
+ * One panel of the reference stream (ppos/pval, pos_len entries; positions
+ * are row*256 + col inside the panel), codebook `table` of valid_table_size+1
+ * floats.  variant: 0 = sblas_kernel_operation, 1 = _naive (A m x k lda,
+ * C m x n ldc), 2 = _trans, 3 = _trans_ex (A^T k x lda, C^T n x ldc). */
+SM_API sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t k,
+                                 const float *a, int32_t lda, float *c, int32_t ldc, float alpha,
+                                 const uint8_t *ppos, const uint8_t *pval, int32_t pos_len,
+                                 const float *table, int32_t valid_table_size, sm_stream stream);
+
+/* Synchronise the stream and report asynchronous kernel errors. */
+SM_API sm_status sm_stream_sync(sm_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPARSEMATRIX_AMD_H */

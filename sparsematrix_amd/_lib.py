@@ -1,0 +1,132 @@
+"""ctypes binding of the C ABI in include/sparsematrix.h.
+
+The shared library is built in-tree (``make`` / ``__graft_entry__.build()``) as
+``sparsematrix_amd/libsparsematrix_amd.so``.  There is no fallback: if the
+library is missing or fails to load, every entry point raises.
+
+HIP runtime note: PyTorch-ROCm ships its own ``libamdhip64.so`` (SONAME
+``libamdhip64.so.7``).  When torch is importable it is imported *before* the
+library is opened so that the already-loaded runtime satisfies the library's
+``libamdhip64.so.7`` dependency and one process holds one HIP runtime.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsparsematrix_amd.so")
+
+# sm_status
+SM_OK = 0
+SM_ERR_INVALID_ARG = 1
+SM_ERR_OUT_OF_MEMORY = 2
+SM_ERR_HIP = 3
+SM_ERR_NOT_SUPPORTED = 4
+SM_ERR_TOO_LARGE = 5
+SM_ERR_INVALID_MATRIX = 6
+SM_ERR_NO_DEVICE = 7
+
+# sm_trans / sm_algo
+SM_NO_TRANS, SM_TRANS = 0, 1
+ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3}
+
+# Every symbol include/sparsematrix.h declares (tests check the .so exports them).
+EXPORTS = (
+    "sm_version", "sm_status_string", "sm_last_error", "sm_device_count",
+    "sm_create_from_dense_index", "sm_create_from_csr", "sm_create_from_csr_device",
+    "sm_destroy", "sm_get_info", "sm_num_rows", "sm_num_cols", "sm_copy_ref_stream",
+    "sm_copy_csr", "sm_to_dense", "sm_equal", "sm_spmv", "sm_spmm", "sm_addmatmat",
+    "sm_addmatmat_host", "sm_beta_scale", "sm_transpose", "sm_panel_kernel", "sm_stream_sync",
+)
+
+
+class SmInfo(C.Structure):
+    _fields_ = [
+        ("s_rows", C.c_int64), ("s_cols", C.c_int64), ("n_rows", C.c_int64),
+        ("n_cols", C.c_int64), ("nnz", C.c_int64), ("table_size", C.c_int32),
+        ("has_ref_stream", C.c_int32), ("n_entries", C.c_int64), ("n_panels", C.c_int64),
+        ("device", C.c_int32), ("n_tiles", C.c_int32), ("n_long_rows", C.c_int32),
+        ("max_row_nnz", C.c_int32), ("device_bytes", C.c_int64),
+    ]
+
+
+class SparseMatrixError(RuntimeError):
+    def __init__(self, status: int, where: str, message: str):
+        self.status = status
+        super().__init__(f"{where}: status {status}: {message}")
+
+
+_lib = None
+_lock = threading.Lock()
+
+_vp, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+
+
+def _declare(L):
+    sig = {
+        "sm_version": ([], C.c_char_p),
+        "sm_status_string": ([C.c_int], C.c_char_p),
+        "sm_last_error": ([], C.c_char_p),
+        "sm_device_count": ([C.POINTER(_i32)], C.c_int),
+        "sm_create_from_dense_index": ([_vp, _i32, _i32, _i32, _vp, _i32, C.c_int, _i32,
+                                        C.POINTER(_vp)], C.c_int),
+        "sm_create_from_csr": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, C.POINTER(_vp)], C.c_int),
+        "sm_create_from_csr_device": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp,
+                                       C.POINTER(_vp)], C.c_int),
+        "sm_destroy": ([_vp], None),
+        "sm_get_info": ([_vp, C.POINTER(SmInfo)], C.c_int),
+        "sm_num_rows": ([_vp], _i32),
+        "sm_num_cols": ([_vp], _i32),
+        "sm_copy_ref_stream": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+        "sm_copy_csr": ([_vp, _vp, _vp, _vp], C.c_int),
+        "sm_to_dense": ([_vp, _vp, _i32, C.c_int], C.c_int),
+        "sm_equal": ([_vp, _vp], _i32),
+        "sm_spmv": ([_vp, _f32, _vp, _f32, _vp, C.c_int, _vp], C.c_int),
+        "sm_spmm": ([_vp, _i32, _f32, _vp, _i64, _f32, _vp, _i64, C.c_int, _vp], C.c_int),
+        "sm_addmatmat": ([_vp, _vp, _i32, _i32, _vp, _i32, _f32, _f32, C.c_int, _vp], C.c_int),
+        "sm_addmatmat_host": ([_vp, _vp, _i32, _i32, _vp, _i32, _f32, _f32], C.c_int),
+        "sm_beta_scale": ([_vp, _i32, _i32, _i32, _f32, _vp], C.c_int),
+        "sm_transpose": ([_vp, _i32, _i32, _i32, _vp, _i32, _vp], C.c_int),
+        "sm_panel_kernel": ([_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp, _i32,
+                             _vp, _i32, _vp], C.c_int),
+        "sm_stream_sync": ([_vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def load(path: str | None = None):
+    """Open the in-tree library (raises if it is missing: there is no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError(
+                f"{p} not found: build it with `make` (or __graft_entry__.build()); "
+                "sparsematrix_amd has no CPU fallback")
+        try:  # one HIP runtime per process: let torch's libamdhip64 load first
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is part of this image
+            pass
+        L = C.CDLL(p, mode=C.RTLD_GLOBAL)
+        _declare(L)
+        _lib = L
+        return L
+
+
+def check(status: int, where: str) -> None:
+    if status != SM_OK:
+        L = load()
+        raise SparseMatrixError(status, where, (L.sm_last_error() or b"").decode())
+
+
+def device_count() -> int:
+    n = _i32(0)
+    load().sm_device_count(C.byref(n))
+    return int(n.value)

@@ -1,0 +1,598 @@
+// capi.cpp -- the extern "C" boundary of libsparsematrix_amd.so
+// (include/sparsematrix.h).  Host-side C++: argument checks, device memory,
+// uploads, planning and kernel dispatch.  All arithmetic runs in the HIP
+// kernels of kernels.hip; there is no CPU compute path.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <string>
+
+#include "encode.h"
+#include "sm_internal.h"
+
+using namespace smamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+sm_status fail(sm_status s, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return s;
+}
+
+sm_status hip_fail(hipError_t e, const char *what) {
+    return fail(e == hipErrorOutOfMemory ? SM_ERR_OUT_OF_MEMORY : SM_ERR_HIP, "%s: %s (%d)", what,
+                hipGetErrorString(e), (int)e);
+}
+
+#define SM_TRY_HIP(call)                                    \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return hip_fail(e_, #call);   \
+    } while (0)
+
+constexpr int64_t kI32Max = std::numeric_limits<int32_t>::max();
+
+// Makes `dev` current for the scope and restores the caller's device.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+hipError_t dev_alloc(T **p, int64_t count, int64_t &acct) {
+    const size_t bytes = (size_t)std::max<int64_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void **)p, bytes);
+    if (e == hipSuccess) acct += (int64_t)bytes;
+    return e;
+}
+
+void free_device(sm_matrix *m) {
+    DeviceGuard g(m->device);
+    (void)hipFree(m->d_row_ptr);
+    (void)hipFree(m->d_col);
+    (void)hipFree(m->d_val);
+    (void)hipFree(m->plan.d_tiles);
+    (void)hipFree(m->plan.d_long_rows);
+    (void)hipFree(m->plan.d_long_ptr);
+    (void)hipFree(m->plan.d_chunks);
+    m->d_row_ptr = m->d_col = nullptr;
+    m->d_val = nullptr;
+    m->plan = Plan();
+}
+
+// Build the stream plan from a host row_ptr and upload it.
+sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
+    PlanHost ph;
+    plan_rows(rp_host, m->n_rows, kTileNnz, kTileRows, kLongChunk, kSerialRowMax, ph);
+    std::vector<Tile> tiles(ph.tiles.size());
+    for (size_t i = 0; i < tiles.size(); i++)
+        tiles[i] = Tile{ph.tiles[i].r0, ph.tiles[i].r1, ph.tiles[i].flags, 0};
+    std::vector<Chunk> chunks(ph.chunks.size());
+    for (size_t i = 0; i < chunks.size(); i++)
+        chunks[i] = Chunk{ph.chunks[i].lr, ph.chunks[i].begin, ph.chunks[i].end, 0};
+    Plan &p = m->plan;
+    p.n_tiles = (int32_t)tiles.size();
+    p.n_long = (int32_t)ph.long_rows.size();
+    p.n_chunks = (int32_t)chunks.size();
+    p.max_row_nnz = ph.max_row_nnz;
+    p.avg_row_nnz = ph.avg_row_nnz;
+    SM_TRY_HIP(dev_alloc(&p.d_tiles, p.n_tiles, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_chunks, p.n_chunks, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_long_rows, p.n_long, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_long_ptr, p.n_long + 1, m->device_bytes));
+    if (p.n_tiles)
+        SM_TRY_HIP(hipMemcpy(p.d_tiles, tiles.data(), tiles.size() * sizeof(Tile), hipMemcpyHostToDevice));
+    if (p.n_chunks)
+        SM_TRY_HIP(hipMemcpy(p.d_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice));
+    if (p.n_long) {
+        SM_TRY_HIP(hipMemcpy(p.d_long_rows, ph.long_rows.data(), ph.long_rows.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(p.d_long_ptr, ph.long_ptr.data(), ph.long_ptr.size() * 4, hipMemcpyHostToDevice));
+    }
+    return SM_OK;
+}
+
+// Allocate the CSR arrays (col/val carry a zeroed tail of kPadElems for the
+// aligned 16-byte loads of the stream kernel).
+sm_status alloc_csr(sm_matrix *m) {
+    SM_TRY_HIP(dev_alloc(&m->d_row_ptr, m->n_rows + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&m->d_col, m->nnz + kPadElems, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&m->d_val, m->nnz + kPadElems, m->device_bytes));
+    SM_TRY_HIP(hipMemset(m->d_col + m->nnz, 0, kPadElems * sizeof(int32_t)));
+    SM_TRY_HIP(hipMemset(m->d_val + m->nnz, 0, kPadElems * sizeof(float)));
+    return SM_OK;
+}
+
+sm_status check_sizes(int64_t n_rows, int64_t n_cols, int64_t nnz) {
+    if (n_rows < 0 || n_cols < 0 || nnz < 0) return fail(SM_ERR_INVALID_ARG, "negative size");
+    if (n_rows >= kI32Max || n_cols >= kI32Max || nnz >= kI32Max - kPadElems)
+        return fail(SM_ERR_TOO_LARGE, "rows/cols/nnz must be < 2^31 (int32 indexing)");
+    return SM_OK;
+}
+
+sm_status check_device(int32_t device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(SM_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(SM_ERR_INVALID_ARG, "device %d out of range", device);
+    return SM_OK;
+}
+
+// Common tail of the host-CSR constructors.
+sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *col,
+                               const float *val) {
+    sm_status st = alloc_csr(m);
+    if (st != SM_OK) return st;
+    SM_TRY_HIP(hipMemcpy(m->d_row_ptr, rp, (size_t)(m->n_rows + 1) * 4, hipMemcpyHostToDevice));
+    if (m->nnz) {
+        SM_TRY_HIP(hipMemcpy(m->d_col, col, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(m->d_val, val, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
+    }
+    return upload_plan(m, rp);
+}
+
+std::unique_ptr<sm_matrix> new_matrix(int32_t device) {
+    std::unique_ptr<sm_matrix> m(new sm_matrix());
+    m->device = device;
+    return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *sm_version(void) { return "sparsematrix_amd 0.1 (gfx950)"; }
+
+const char *sm_status_string(sm_status s) {
+    switch (s) {
+    case SM_OK: return "ok";
+    case SM_ERR_INVALID_ARG: return "invalid argument";
+    case SM_ERR_OUT_OF_MEMORY: return "out of memory";
+    case SM_ERR_HIP: return "HIP runtime error";
+    case SM_ERR_NOT_SUPPORTED: return "not supported";
+    case SM_ERR_TOO_LARGE: return "too large for int32 indexing";
+    case SM_ERR_INVALID_MATRIX: return "invalid matrix";
+    case SM_ERR_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown status";
+}
+
+const char *sm_last_error(void) { return g_err.c_str(); }
+
+sm_status sm_device_count(int32_t *count) {
+    if (!count) return fail(SM_ERR_INVALID_ARG, "count is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return n ? SM_OK : fail(SM_ERR_NO_DEVICE, "no HIP device visible");
+}
+
+void sm_destroy(sm_matrix *m) {
+    if (!m) return;
+    free_device(m);
+    delete m;
+}
+
+sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t cols,
+                                     int32_t stride, const float *table, int32_t table_size,
+                                     sm_trans trans, int32_t device, sm_matrix **out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    if (table_size < 0 || table_size > 255)
+        return fail(SM_ERR_INVALID_ARG, "table_size %d not in [0, 255]", table_size);
+    if (rows < 0 || cols < 0 || stride < cols)
+        return fail(SM_ERR_INVALID_ARG, "bad shape rows=%d cols=%d stride=%d", rows, cols, stride);
+    if (trans != SM_NO_TRANS && trans != SM_TRANS) return fail(SM_ERR_INVALID_ARG, "bad trans");
+    if (table_size > 0 && rows > 0 && cols > 0 && (!index || !table))
+        return fail(SM_ERR_INVALID_ARG, "null index/table");
+    sm_status st = check_device(device);
+    if (st != SM_OK) return st;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+
+    EncodeResult er;
+    if (table_size > 0 && rows > 0 && cols > 0) {
+        if (encode_dense_index(index, rows, cols, stride, table, table_size, trans == SM_TRANS, er))
+            return fail(SM_ERR_INVALID_ARG, "encode failed");
+    } else if (table_size > 0) {
+        // degenerate shape: the reference still records rows_/cols_ (:63-64, :96-97)
+        er.s_rows = trans == SM_TRANS ? cols : rows;
+        er.s_cols = trans == SM_TRANS ? rows : cols;
+        er.table.assign(table, table + table_size);
+        er.table.push_back(0.0f);
+        er.table_size = table_size;
+        er.row_ptr.assign((size_t)er.s_cols + 1, 0);
+    } else {
+        er.row_ptr.assign(1, 0);   // val_table_size == 0: empty 0 x 0 (:26)
+    }
+    const int64_t nnz = er.row_ptr.back();
+    st = check_sizes(er.s_cols, er.s_rows, nnz);
+    if (st != SM_OK) return st;
+
+    auto m = new_matrix(device);
+    m->n_rows = er.s_cols;
+    m->n_cols = er.s_rows;
+    m->nnz = nnz;
+    m->s_rows = er.s_rows;
+    m->s_cols = er.s_cols;
+    m->has_ref = true;   // the reference encoding exists (possibly empty)
+    m->table_size = er.table_size;
+    m->table = std::move(er.table);
+    m->pos = std::move(er.pos);
+    m->val = std::move(er.val_id);
+    m->panel_row_off = std::move(er.panel_row_off);
+    m->panel_col_off = std::move(er.panel_col_off);
+    m->panel_begin = std::move(er.panel_begin);
+    m->panel_end = std::move(er.panel_end);
+    std::vector<int32_t> rp32(er.row_ptr.size());
+    for (size_t i = 0; i < rp32.size(); i++) rp32[i] = (int32_t)er.row_ptr[i];
+    st = finish_from_host_csr(m.get(), rp32.data(), er.col.data(), er.val.data());
+    if (st != SM_OK) {
+        free_device(m.get());
+        return st;
+    }
+    *out = m.release();
+    return SM_OK;
+}
+
+sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *row_ptr,
+                             const int32_t *col_idx, const float *val, int32_t device,
+                             sm_matrix **out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    sm_status st = check_sizes(n_rows, n_cols, nnz);
+    if (st != SM_OK) return st;
+    if (!row_ptr || (nnz > 0 && (!col_idx || !val)))
+        return fail(SM_ERR_INVALID_ARG, "null CSR array");
+    // host validation: monotone row_ptr, columns in range
+    if (row_ptr[0] != 0 || row_ptr[n_rows] != nnz)
+        return fail(SM_ERR_INVALID_MATRIX, "row_ptr[0] must be 0 and row_ptr[n] == nnz");
+    for (int64_t r = 0; r < n_rows; r++)
+        if (row_ptr[r + 1] < row_ptr[r])
+            return fail(SM_ERR_INVALID_MATRIX, "row_ptr decreases at row %lld", (long long)r);
+    for (int64_t e = 0; e < nnz; e++)
+        if (col_idx[e] < 0 || col_idx[e] >= n_cols)
+            return fail(SM_ERR_INVALID_MATRIX, "col_idx[%lld] = %d out of range", (long long)e,
+                        col_idx[e]);
+    st = check_device(device);
+    if (st != SM_OK) return st;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    auto m = new_matrix(device);
+    m->n_rows = n_rows;
+    m->n_cols = n_cols;
+    m->nnz = nnz;
+    m->s_rows = n_cols;
+    m->s_cols = n_rows;
+    st = finish_from_host_csr(m.get(), row_ptr, col_idx, val);
+    if (st != SM_OK) {
+        free_device(m.get());
+        return st;
+    }
+    *out = m.release();
+    return SM_OK;
+}
+
+sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                    const int32_t *d_row_ptr, const int32_t *d_col_idx,
+                                    const float *d_val, int32_t device, sm_stream stream,
+                                    sm_matrix **out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    sm_status st = check_sizes(n_rows, n_cols, nnz);
+    if (st != SM_OK) return st;
+    if (!d_row_ptr || (nnz > 0 && (!d_col_idx || !d_val)))
+        return fail(SM_ERR_INVALID_ARG, "null CSR array");
+    st = check_device(device);
+    if (st != SM_OK) return st;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipStream_t s = (hipStream_t)stream;
+    auto m = new_matrix(device);
+    m->n_rows = n_rows;
+    m->n_cols = n_cols;
+    m->nnz = nnz;
+    m->s_rows = n_cols;
+    m->s_cols = n_rows;
+    st = alloc_csr(m.get());
+    if (st != SM_OK) { free_device(m.get()); return st; }
+    hipError_t e = hipMemcpyAsync(m->d_row_ptr, d_row_ptr, (size_t)(n_rows + 1) * 4,
+                                  hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess && nnz) {
+        e = hipMemcpyAsync(m->d_col, d_col_idx, (size_t)nnz * 4, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(m->d_val, d_val, (size_t)nnz * 4, hipMemcpyDeviceToDevice, s);
+    }
+    int32_t *d_flag = nullptr;
+    if (e == hipSuccess) e = hipMalloc((void **)&d_flag, sizeof(int32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_flag, 0, sizeof(int32_t), s);
+    if (e == hipSuccess)
+        e = launch_validate((int32_t)n_rows, (int32_t)n_cols, (int32_t)nnz, m->d_row_ptr,
+                            m->d_col, d_flag, s);
+    int32_t flag = 0;
+    std::vector<int32_t> rp((size_t)n_rows + 1);
+    if (e == hipSuccess) e = hipMemcpyAsync(&flag, d_flag, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(rp.data(), m->d_row_ptr, rp.size() * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d_flag);
+    if (e != hipSuccess) {
+        free_device(m.get());
+        return hip_fail(e, "sm_create_from_csr_device");
+    }
+    if (flag) {
+        free_device(m.get());
+        return fail(SM_ERR_INVALID_MATRIX, "device CSR failed validation (flags 0x%x)", flag);
+    }
+    st = upload_plan(m.get(), rp.data());
+    if (st != SM_OK) { free_device(m.get()); return st; }
+    *out = m.release();
+    return SM_OK;
+}
+
+sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
+    if (!m || !info) return fail(SM_ERR_INVALID_ARG, "null argument");
+    info->s_rows = m->s_rows;
+    info->s_cols = m->s_cols;
+    info->n_rows = m->n_rows;
+    info->n_cols = m->n_cols;
+    info->nnz = m->nnz;
+    info->table_size = m->table_size;
+    info->has_ref_stream = m->has_ref ? 1 : 0;
+    info->n_entries = (int64_t)m->pos.size();
+    info->n_panels = (int64_t)m->panel_col_off.size();
+    info->device = m->device;
+    info->n_tiles = m->plan.n_tiles;
+    info->n_long_rows = m->plan.n_long;
+    info->max_row_nnz = m->plan.max_row_nnz;
+    info->device_bytes = m->device_bytes;
+    return SM_OK;
+}
+
+int32_t sm_num_rows(const sm_matrix *m) { return m ? (int32_t)m->s_rows : 0; }
+int32_t sm_num_cols(const sm_matrix *m) { return m ? (int32_t)m->s_cols : 0; }
+
+sm_status sm_copy_ref_stream(const sm_matrix *m, uint8_t *pos, uint8_t *val, int32_t *pro,
+                             int32_t *pco, int64_t *pb, int64_t *pe) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    if (!m->has_ref) return fail(SM_ERR_NOT_SUPPORTED, "matrix holds no reference encoding");
+    if (pos && !m->pos.empty()) memcpy(pos, m->pos.data(), m->pos.size());
+    if (val && !m->val.empty()) memcpy(val, m->val.data(), m->val.size());
+    const size_t P = m->panel_col_off.size();
+    if (pro && P) memcpy(pro, m->panel_row_off.data(), P * 4);
+    if (pco && P) memcpy(pco, m->panel_col_off.data(), P * 4);
+    if (pb && P) memcpy(pb, m->panel_begin.data(), P * 8);
+    if (pe && P) memcpy(pe, m->panel_end.data(), P * 8);
+    return SM_OK;
+}
+
+sm_status sm_copy_csr(const sm_matrix *m, int32_t *row_ptr, int32_t *col_idx, float *val) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    DeviceGuard g(m->device);
+    if (row_ptr)
+        SM_TRY_HIP(hipMemcpy(row_ptr, m->d_row_ptr, (size_t)(m->n_rows + 1) * 4, hipMemcpyDeviceToHost));
+    if (col_idx && m->nnz)
+        SM_TRY_HIP(hipMemcpy(col_idx, m->d_col, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
+    if (val && m->nnz)
+        SM_TRY_HIP(hipMemcpy(val, m->d_val, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
+    return SM_OK;
+}
+
+sm_status sm_to_dense(const sm_matrix *m, float *out, int32_t stride, sm_trans trans) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    if (trans != SM_NO_TRANS && trans != SM_TRANS) return fail(SM_ERR_INVALID_ARG, "bad trans");
+    // NoTrans: S, s_rows x stride (s_cols used); Trans: S^T = B, s_cols x stride (s_rows used)
+    const int64_t out_rows = trans == SM_TRANS ? m->s_cols : m->s_rows;
+    const int64_t width = trans == SM_TRANS ? m->s_rows : m->s_cols;
+    if (out_rows == 0) return SM_OK;
+    if (!out || stride < width) return fail(SM_ERR_INVALID_ARG, "null out or stride < %lld", (long long)width);
+    DeviceGuard g(m->device);
+    const size_t bytes = (size_t)out_rows * stride * sizeof(float);
+    float *d = nullptr;
+    SM_TRY_HIP(hipMalloc((void **)&d, bytes));
+    hipError_t e = hipMemsetAsync(d, 0, bytes, 0);
+    if (e == hipSuccess)
+        e = launch_scatter_dense((int32_t)m->n_rows, m->d_row_ptr, m->d_col, m->d_val, d, stride,
+                                 trans == SM_TRANS, 0);
+    if (e == hipSuccess) e = hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "sm_to_dense");
+    return SM_OK;
+}
+
+int32_t sm_equal(const sm_matrix *a, const sm_matrix *b) {
+    if (!a || !b) return 0;
+    if (a == b) return 1;
+    if (a->s_rows != b->s_rows || a->s_cols != b->s_cols || a->nnz != b->nnz) return 0;
+    if (a->has_ref && b->has_ref) {
+        // the reference's own member-wise comparison (sparse-matrix.cc:197-207)
+        if (a->table.size() != b->table.size() ||
+            memcmp(a->table.data(), b->table.data(), a->table.size() * 4) != 0)
+            return 0;
+        return a->pos == b->pos && a->val == b->val && a->panel_row_off == b->panel_row_off &&
+               a->panel_col_off == b->panel_col_off && a->panel_begin == b->panel_begin &&
+               a->panel_end == b->panel_end;
+    }
+    std::vector<int32_t> ra((size_t)a->n_rows + 1), rb((size_t)b->n_rows + 1);
+    std::vector<int32_t> ca((size_t)a->nnz), cb((size_t)b->nnz);
+    std::vector<float> va((size_t)a->nnz), vb((size_t)b->nnz);
+    if (sm_copy_csr(a, ra.data(), ca.data(), va.data()) != SM_OK) return 0;
+    if (sm_copy_csr(b, rb.data(), cb.data(), vb.data()) != SM_OK) return 0;
+    return ra == rb && ca == cb &&
+           (va.empty() || memcmp(va.data(), vb.data(), va.size() * 4) == 0);
+}
+
+// ---------------------------------------------------------------------------
+sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, float *y,
+                  sm_algo algo, sm_stream stream) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    if (m->n_rows == 0) return SM_OK;
+    if (!y || (alpha != 0.0f && m->n_cols > 0 && !x)) return fail(SM_ERR_INVALID_ARG, "null x/y");
+    DeviceGuard g(m->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t n = (int32_t)m->n_rows;
+    hipError_t e = hipSuccess;
+    if (alpha == 0.0f) {   // sparse-matrix.cc:149-152: only the beta pass
+        if (beta != 1.0f) e = launch_beta(y, 1, n, n, beta, s);
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv beta");
+    }
+    switch (algo) {
+    case SM_ALGO_PARITY:
+        e = launch_spmv_parity(n, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta, s);
+        break;
+    case SM_ALGO_VECTOR:
+        e = launch_spmv_vector(n, m->plan.avg_row_nnz, m->d_row_ptr, m->d_col, m->d_val, x, y,
+                               alpha, beta, s);
+        break;
+    case SM_ALGO_AUTO:
+    case SM_ALGO_STREAM: {
+        float *partials = nullptr;
+        if (m->plan.n_long) {
+            e = hipMallocAsync((void **)&partials, (size_t)m->plan.n_chunks * sizeof(float), s);
+            if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
+        }
+        e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
+                               partials, s);
+        if (partials) {
+            hipError_t e2 = hipFreeAsync(partials, s);
+            if (e == hipSuccess) e = e2;
+        }
+        break;
+    }
+    default:
+        return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
+    }
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv launch");
+}
+
+sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X, int64_t ldx,
+                  float beta, float *Y, int64_t ldy, sm_algo algo, sm_stream stream) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    if (n_rhs < 0) return fail(SM_ERR_INVALID_ARG, "n_rhs < 0");
+    if (m->n_rows == 0 || n_rhs == 0) return SM_OK;
+    if (ldy < n_rhs || ldx < n_rhs) return fail(SM_ERR_INVALID_ARG, "ldx/ldy < n_rhs");
+    if (!Y || (alpha != 0.0f && m->n_cols > 0 && !X)) return fail(SM_ERR_INVALID_ARG, "null X/Y");
+    DeviceGuard g(m->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t n = (int32_t)m->n_rows;
+    hipError_t e;
+    if (alpha == 0.0f) {
+        e = beta != 1.0f ? launch_beta(Y, n, n_rhs, ldy, beta, s) : hipSuccess;
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmm beta");
+    }
+    const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
+                        ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
+    if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
+        e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, X, ldx, Y, ldy, alpha,
+                                 beta, s);
+    else if (algo >= SM_ALGO_AUTO && algo <= SM_ALGO_VECTOR)
+        e = launch_spmm_generic(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, X, ldx, 1, Y, ldy, 1,
+                                alpha, beta, true, s);
+    else
+        return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmm launch");
+}
+
+sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t lda, float *c,
+                       int32_t ldc, float alpha, float beta, sm_algo algo, sm_stream stream) {
+    if (!mat) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    const int64_t k = mat->s_rows, n = mat->s_cols;
+    if (m < 0) return fail(SM_ERR_INVALID_ARG, "m < 0");
+    if (m == 0 || n == 0) return SM_OK;
+    if (ldc < n || (alpha != 0.0f && lda < k)) return fail(SM_ERR_INVALID_ARG, "lda/ldc too small");
+    if (!c || (alpha != 0.0f && k > 0 && !a)) return fail(SM_ERR_INVALID_ARG, "null a/c");
+    if (m == 1) return sm_spmv(mat, alpha, a, beta, c, algo, stream);
+    DeviceGuard g(mat->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    if (alpha == 0.0f) {
+        e = beta != 1.0f ? launch_beta(c, m, (int32_t)n, ldc, beta, s) : hipSuccess;
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat beta");
+    }
+    // C^T = B A^T, read in place: X(kk, i) = a[i*lda + kk], Y(j, i) = c[i*ldc + j]
+    e = launch_spmm_generic((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val, a, 1, lda, c,
+                            1, ldc, alpha, beta, false, s);
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat launch");
+}
+
+sm_status sm_addmatmat_host(const sm_matrix *mat, const float *a, int32_t m, int32_t lda, float *c,
+                            int32_t ldc, float alpha, float beta) {
+    if (!mat) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    const int64_t k = mat->s_rows, n = mat->s_cols;
+    if (m < 0) return fail(SM_ERR_INVALID_ARG, "m < 0");
+    if (m == 0 || n == 0) return SM_OK;
+    if (ldc < n || (alpha != 0.0f && lda < k)) return fail(SM_ERR_INVALID_ARG, "lda/ldc too small");
+    if (!c || (alpha != 0.0f && k > 0 && !a)) return fail(SM_ERR_INVALID_ARG, "null a/c");
+    DeviceGuard g(mat->device);
+    const int64_t a_elems = (alpha != 0.0f && k > 0) ? (int64_t)(m - 1) * lda + k : 0;
+    const int64_t c_elems = (int64_t)(m - 1) * ldc + n;
+    float *da = nullptr, *dc = nullptr;
+    hipError_t e = hipSuccess;
+    if (a_elems) e = hipMalloc((void **)&da, (size_t)a_elems * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&dc, (size_t)c_elems * 4);
+    if (e == hipSuccess && a_elems) e = hipMemcpy(da, a, (size_t)a_elems * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, c, (size_t)c_elems * 4, hipMemcpyHostToDevice);
+    sm_status st = SM_OK;
+    if (e == hipSuccess) {
+        st = sm_addmatmat(mat, da, m, lda, dc, ldc, alpha, beta, SM_ALGO_PARITY, nullptr);
+        if (st == SM_OK) e = hipMemcpy(c, dc, (size_t)c_elems * 4, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(da);
+    (void)hipFree(dc);
+    if (st != SM_OK) return st;
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat_host");
+}
+
+sm_status sm_beta_scale(float *c, int32_t m, int32_t n, int32_t ldc, float beta, sm_stream stream) {
+    if (m < 0 || n < 0 || (m > 0 && ldc < n)) return fail(SM_ERR_INVALID_ARG, "bad shape");
+    if ((int64_t)m * n == 0) return SM_OK;
+    if (!c) return fail(SM_ERR_INVALID_ARG, "null c");
+    hipError_t e = launch_beta(c, m, n, ldc, beta, (hipStream_t)stream);
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_beta_scale");
+}
+
+sm_status sm_transpose(const float *a, int32_t m, int32_t n, int32_t lda, float *sa, int32_t ldsa,
+                       sm_stream stream) {
+    if (m < 0 || n < 0 || (m > 0 && lda < n) || (n > 0 && ldsa < m))
+        return fail(SM_ERR_INVALID_ARG, "bad shape");   // kernel.cc:33 asserts ldsa >= m
+    if ((int64_t)m * n == 0) return SM_OK;
+    if (!a || !sa) return fail(SM_ERR_INVALID_ARG, "null pointer");
+    hipError_t e = launch_transpose(a, m, n, lda, sa, ldsa, (hipStream_t)stream);
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_transpose");
+}
+
+sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t k, const float *a,
+                          int32_t lda, float *c, int32_t ldc, float alpha, const uint8_t *ppos,
+                          const uint8_t *pval, int32_t pos_len, const float *table,
+                          int32_t valid_table_size, sm_stream stream) {
+    (void)variant; (void)m; (void)n; (void)k; (void)a; (void)lda; (void)c; (void)ldc;
+    (void)alpha; (void)ppos; (void)pval; (void)pos_len; (void)table; (void)valid_table_size;
+    (void)stream;
+    return fail(SM_ERR_NOT_SUPPORTED, "sm_panel_kernel: reference-format kernels not built yet");
+}
+
+sm_status sm_stream_sync(sm_stream stream) {
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_stream_sync");
+}
+
+}  // extern "C"

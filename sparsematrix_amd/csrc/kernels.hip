@@ -1,0 +1,469 @@
+// kernels.hip -- gfx950 kernels of libsparsematrix_amd.so.
+//
+// Everything here is HBM-bound integer/fp32 streaming: no MFMA.  The design
+// (DESIGN.md "Kernels") in one line per kernel:
+//   spmv_parity      one thread per row, terms added in stored order with
+//                    separate round-to-nearest mul/add: bit-identical to the
+//                    reference's generic-C AddMatMat (kernel.cc:568-582, 791).
+//   spmv_stream      nnz-balanced row tiles (<= 4096 terms): aligned 16-byte
+//                    loads of col/val, x gathered, terms staged in LDS, then
+//                    each short row summed by one thread in stored order
+//                    (bit-exact), rows > 64 terms by a wavefront (DPP/shuffle
+//                    tree), rows > 4096 terms split across workgroups with a
+//                    deterministic ordered finalize.
+//   spmv_vector      CSR-vector: L lanes per row (L = pow2 near the mean row
+//                    length), shuffle reduction.
+//   spmm_rowpanel    N right-hand sides, row-major X/Y: N/4 lanes per row own
+//                    a float4 slice of the output row; the row's (col, val)
+//                    pairs are loaded cooperatively and broadcast by shuffle;
+//                    every output element accumulates in stored order
+//                    (bit-exact).
+//   spmm_generic     any N and any X/Y strides (AddMatMat layouts), one thread
+//                    per output element, stored order (bit-exact).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (Makefile).
+#include "sm_internal.h"
+
+namespace smamd {
+namespace {
+
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+// One term of the reference: a * (table_value * alpha) (kernel.cc:791, 580-582).
+__device__ __forceinline__ float term(float xv, float v, float alpha) {
+    return mul_rn(xv, mul_rn(v, alpha));
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+// Streamed (read-once) 16-byte loads of val/col.  SM_NT_LOADS selects the
+// non-temporal cache policy (measured both ways).
+#ifndef SM_NT_LOADS
+#define SM_NT_LOADS 0
+#endif
+__device__ __forceinline__ float4 ld_stream(const float4 *p) {
+#if SM_NT_LOADS
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+#else
+    const f32x4 v = *reinterpret_cast<const f32x4 *>(p);
+#endif
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 ld_stream(const int4 *p) {
+#if SM_NT_LOADS
+    const i32x4 v = __builtin_nontemporal_load(reinterpret_cast<const i32x4 *>(p));
+#else
+    const i32x4 v = *reinterpret_cast<const i32x4 *>(p);
+#endif
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ float wave_sum(float s) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s = add_rn(s, __shfl_xor(s, off, 64));
+    return s;
+}
+
+// LDS slot of the l-th staged term: one pad word every 32 keeps the
+// thread-per-row reads (stride = row length) off a single bank.
+__device__ __forceinline__ int lds_slot(int l) { return l + (l >> 5); }
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void spmv_parity_kernel(int32_t n, const int32_t *__restrict__ rp,
+                                                          const int32_t *__restrict__ col,
+                                                          const float *__restrict__ val,
+                                                          const float *__restrict__ x,
+                                                          float *__restrict__ y, float alpha,
+                                                          float beta) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    float acc = y[r];
+    if (beta != 1.0f) acc = mul_rn(acc, beta);
+    const int32_t e1 = rp[r + 1];
+    for (int32_t e = rp[r]; e < e1; ++e) acc = add_rn(acc, term(x[col[e]], val[e], alpha));
+    y[r] = acc;
+}
+
+// ---------------------------------------------------------------------------
+template <int THREADS, int TILE>
+__global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
+    const Tile *__restrict__ tiles, const Chunk *__restrict__ chunks, int32_t n_chunks,
+    const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ x, float *__restrict__ y,
+    float alpha, float beta, float *__restrict__ partials) {
+    constexpr int kLds = TILE + TILE / 32 + 8;
+    constexpr int kWaves = THREADS / 64;
+    __shared__ float prod[kLds];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int32_t b = blockIdx.x;
+
+    if (b < n_chunks) {
+        // ---- one chunk of a long row: tree sum of its terms ----------------
+        const Chunk ch = chunks[b];
+        float s = 0.0f;
+        for (int32_t i = (ch.begin & ~3) + 4 * tid; i < ch.end; i += 4 * THREADS) {
+            const float4 v = ld_stream(reinterpret_cast<const float4 *>(val + i));
+            const int4 c = ld_stream(reinterpret_cast<const int4 *>(col + i));
+            if (i + 0 >= ch.begin && i + 0 < ch.end) s = add_rn(s, term(x[c.x], v.x, alpha));
+            if (i + 1 >= ch.begin && i + 1 < ch.end) s = add_rn(s, term(x[c.y], v.y, alpha));
+            if (i + 2 >= ch.begin && i + 2 < ch.end) s = add_rn(s, term(x[c.z], v.z, alpha));
+            if (i + 3 >= ch.begin && i + 3 < ch.end) s = add_rn(s, term(x[c.w], v.w, alpha));
+        }
+        s = wave_sum(s);
+        if (lane == 0) prod[wave] = s;
+        __syncthreads();
+        if (tid == 0) {
+            float t = prod[0];
+#pragma unroll
+            for (int w = 1; w < kWaves; ++w) t = add_rn(t, prod[w]);
+            partials[b] = t;
+        }
+        return;
+    }
+
+    // ---- a tile of short rows -----------------------------------------------
+    const Tile t = tiles[b - n_chunks];
+    const int32_t s0 = rp[t.r0];
+    const int32_t e0 = rp[t.r1];
+    const int32_t base = s0 & ~3;
+    constexpr int kIt = TILE / (4 * THREADS) + 1;   // +1: unaligned tile start
+    float4 vv[kIt];
+    int4 cc[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int32_t i = base + 4 * (tid + it * THREADS);
+        if (i < e0) {
+            vv[it] = ld_stream(reinterpret_cast<const float4 *>(val + i));
+            cc[it] = ld_stream(reinterpret_cast<const int4 *>(col + i));
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int32_t i = base + 4 * (tid + it * THREADS);
+        if (i < e0) {
+            const float vq[4] = {vv[it].x, vv[it].y, vv[it].z, vv[it].w};
+            const int32_t cq[4] = {cc[it].x, cc[it].y, cc[it].z, cc[it].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t idx = i + q;
+                if (idx >= s0 && idx < e0) prod[lds_slot(idx - s0)] = term(x[cq[q]], vq[q], alpha);
+            }
+        }
+    }
+    __syncthreads();
+
+    // Short rows: one thread each, terms in stored order (reference order).
+    for (int32_t r = t.r0 + tid; r < t.r1; r += THREADS) {
+        const int32_t a = rp[r] - s0;
+        const int32_t e = rp[r + 1] - s0;
+        if (e - a > kSerialRowMax) continue;
+        float acc = y[r];
+        if (beta != 1.0f) acc = mul_rn(acc, beta);
+        for (int32_t k = a; k < e; ++k) acc = add_rn(acc, prod[lds_slot(k)]);
+        y[r] = acc;
+    }
+    // Medium rows: one wavefront each, shuffle tree.
+    if (t.flags & 1) {
+        for (int32_t r = t.r0 + wave; r < t.r1; r += kWaves) {
+            const int32_t a = rp[r] - s0;
+            const int32_t e = rp[r + 1] - s0;
+            if (e - a <= kSerialRowMax) continue;
+            float s = 0.0f;
+            for (int32_t k = a + lane; k < e; k += 64) s = add_rn(s, prod[lds_slot(k)]);
+            s = wave_sum(s);
+            if (lane == 0) {
+                float acc = y[r];
+                if (beta != 1.0f) acc = mul_rn(acc, beta);
+                y[r] = add_rn(acc, s);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void spmv_long_finalize_kernel(
+    int32_t n_long, const int32_t *__restrict__ long_rows, const int32_t *__restrict__ long_ptr,
+    const float *__restrict__ partials, float *__restrict__ y, float beta) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_long) return;
+    const int32_t r = long_rows[i];
+    float acc = y[r];
+    if (beta != 1.0f) acc = mul_rn(acc, beta);
+    for (int32_t c = long_ptr[i]; c < long_ptr[i + 1]; ++c) acc = add_rn(acc, partials[c]);
+    y[r] = acc;
+}
+
+// ---------------------------------------------------------------------------
+template <int L>
+__global__ __launch_bounds__(256) void spmv_vector_kernel(int32_t n, const int32_t *__restrict__ rp,
+                                                          const int32_t *__restrict__ col,
+                                                          const float *__restrict__ val,
+                                                          const float *__restrict__ x,
+                                                          float *__restrict__ y, float alpha,
+                                                          float beta) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t r = (int32_t)(gid / L);
+    const int lane = (int)(gid % L);
+    if (r >= n) return;   // whole L-lane groups leave together
+    const int32_t e1 = rp[r + 1];
+    float s = 0.0f;
+    for (int32_t e = rp[r] + lane; e < e1; e += L) s = add_rn(s, term(x[col[e]], val[e], alpha));
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) s = add_rn(s, __shfl_xor(s, off, L));
+    if (lane == 0) {
+        float acc = y[r];
+        if (beta != 1.0f) acc = mul_rn(acc, beta);
+        y[r] = add_rn(acc, s);
+    }
+}
+
+// ---------------------------------------------------------------------------
+template <int G>   // lanes per row (power of two); lane g owns rhs [4g, 4g+4)
+__global__ __launch_bounds__(256) void spmm_rowpanel_kernel(
+    int32_t n, int32_t nrhs, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, float alpha, float beta) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t r = (int32_t)(gid / G);
+    const int g = (int)(gid % G);
+    if (r >= n) return;
+    const bool active = 4 * g < nrhs;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float *yp = Y + (int64_t)r * ldy + 4 * g;
+    if (active) acc = *reinterpret_cast<const float4 *>(yp);
+    if (beta != 1.0f) {
+        acc.x = mul_rn(acc.x, beta); acc.y = mul_rn(acc.y, beta);
+        acc.z = mul_rn(acc.z, beta); acc.w = mul_rn(acc.w, beta);
+    }
+    const int32_t a = rp[r];
+    const int32_t e = rp[r + 1];
+    for (int32_t b0 = a; b0 < e; b0 += G) {
+        int32_t myc = 0;
+        float myv = 0.0f;
+        if (b0 + g < e) {
+            myc = col[b0 + g];
+            myv = mul_rn(val[b0 + g], alpha);
+        }
+        const int cnt = min(G, e - b0);
+        float4 xv[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int32_t cj = __shfl(myc, j, G);
+            if (j < cnt && active)
+                xv[j] = *reinterpret_cast<const float4 *>(X + (int64_t)cj * ldx + 4 * g);
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const float vj = __shfl(myv, j, G);
+            if (j < cnt) {
+                acc.x = add_rn(acc.x, mul_rn(xv[j].x, vj));
+                acc.y = add_rn(acc.y, mul_rn(xv[j].y, vj));
+                acc.z = add_rn(acc.z, mul_rn(xv[j].z, vj));
+                acc.w = add_rn(acc.w, mul_rn(xv[j].w, vj));
+            }
+        }
+    }
+    if (active) *reinterpret_cast<float4 *>(yp) = acc;
+}
+
+template <bool RHS_FASTEST>
+__global__ __launch_bounds__(256) void spmm_generic_kernel(
+    int32_t n, int32_t nrhs, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t x_sk, int64_t x_si,
+    float *__restrict__ Y, int64_t y_sj, int64_t y_si, float alpha, float beta) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)n * nrhs) return;
+    int64_t j, i;
+    if (RHS_FASTEST) { j = gid / nrhs; i = gid % nrhs; }
+    else { i = gid / n; j = gid % n; }
+    float *yp = Y + j * y_sj + i * y_si;
+    float acc = *yp;
+    if (beta != 1.0f) acc = mul_rn(acc, beta);
+    const float *xi = X + i * x_si;
+    const int32_t e1 = rp[j + 1];
+    for (int32_t e = rp[j]; e < e1; ++e)
+        acc = add_rn(acc, term(xi[(int64_t)col[e] * x_sk], val[e], alpha));
+    *yp = acc;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void beta_kernel(float *__restrict__ c, int32_t m, int32_t n,
+                                                   int64_t ldc, float beta) {
+    const int64_t total = (int64_t)m * n;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / n, j = t % n;
+        float *p = c + i * ldc + j;
+        *p = mul_rn(*p, beta);
+    }
+}
+
+__global__ __launch_bounds__(256) void transpose_kernel(const float *__restrict__ a, int32_t m,
+                                                        int32_t n, int64_t lda,
+                                                        float *__restrict__ sa, int64_t ldsa,
+                                                        int32_t tiles_n) {
+    __shared__ float tile[64][65];
+    const int32_t tb = blockIdx.x;
+    const int32_t ti = tb / tiles_n, tj = tb % tiles_n;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int k = ty; k < 64; k += 4) {
+        const int64_t i = (int64_t)ti * 64 + k, j = (int64_t)tj * 64 + tx;
+        if (i < m && j < n) tile[k][tx] = a[i * lda + j];
+    }
+    __syncthreads();
+    for (int k = ty; k < 64; k += 4) {
+        const int64_t j = (int64_t)tj * 64 + k, i = (int64_t)ti * 64 + tx;
+        if (i < m && j < n) sa[j * ldsa + i] = tile[tx][k];
+    }
+}
+
+__global__ __launch_bounds__(256) void validate_kernel(int32_t n_rows, int32_t n_cols, int32_t nnz,
+                                                       const int32_t *__restrict__ rp,
+                                                       const int32_t *__restrict__ col,
+                                                       int32_t *flag) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > n_rows) return;
+    if (r == 0 && rp[0] != 0) atomicOr(flag, 1);
+    if (r == n_rows) {
+        if (rp[n_rows] != nnz) atomicOr(flag, 2);
+        return;
+    }
+    const int32_t a = rp[r], e = rp[r + 1];
+    if (a > e || a < 0 || e > nnz) { atomicOr(flag, 4); return; }
+    for (int32_t k = a; k < e; ++k) {
+        const int32_t c = col[k];
+        if (c < 0 || c >= n_cols) { atomicOr(flag, 8); return; }
+    }
+}
+
+__global__ __launch_bounds__(256) void scatter_dense_kernel(int32_t n, const int32_t *__restrict__ rp,
+                                                            const int32_t *__restrict__ col,
+                                                            const float *__restrict__ val,
+                                                            float *__restrict__ out, int64_t stride,
+                                                            bool b_layout) {
+    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+        const int64_t c = col[e];
+        if (b_layout) out[(int64_t)r * stride + c] = val[e];
+        else out[c * stride + r] = val[e];
+    }
+}
+
+inline unsigned blocks_for(int64_t work, int per = 256) {
+    return (unsigned)((work + per - 1) / per);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+hipError_t launch_spmv_parity(int32_t n, const int32_t *rp, const int32_t *col, const float *val,
+                              const float *x, float *y, float alpha, float beta, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(spmv_parity_kernel, dim3(blocks_for(n)), dim3(256), 0, s, n, rp, col, val,
+                       x, y, alpha, beta);
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *col,
+                              const float *val, const float *x, float *y, float alpha,
+                              float beta, float *partials, hipStream_t s) {
+    const int64_t grid = (int64_t)p.n_chunks + p.n_tiles;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, kTileNnz>), dim3((unsigned)grid),
+                       dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, col, val,
+                       x, y, alpha, beta, partials);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.n_long == 0) return e;
+    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.n_long)), dim3(256), 0, s,
+                       p.n_long, p.d_long_rows, p.d_long_ptr, partials, y, beta);
+    return hipGetLastError();
+}
+
+hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
+                              const float *val, const float *x, float *y, float alpha, float beta,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int L = 2;
+    while (L < 64 && L < avg_row) L <<= 1;
+    const unsigned grid = blocks_for((int64_t)n * L);
+#define SM_VEC(LL)                                                                        \
+    case LL:                                                                              \
+        hipLaunchKernelGGL(spmv_vector_kernel<LL>, dim3(grid), dim3(256), 0, s, n, rp, col, \
+                           val, x, y, alpha, beta);                                        \
+        break;
+    switch (L) { SM_VEC(2) SM_VEC(4) SM_VEC(8) SM_VEC(16) SM_VEC(32) SM_VEC(64) }
+#undef SM_VEC
+    return hipGetLastError();
+}
+
+hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
+                               const float *val, const float *X, int64_t x_sk, int64_t x_si,
+                               float *Y, int64_t y_sj, int64_t y_si, float alpha, float beta,
+                               bool rhs_fastest, hipStream_t s) {
+    const int64_t total = (int64_t)n * nrhs;
+    if (total <= 0) return hipSuccess;
+    if (rhs_fastest)
+        hipLaunchKernelGGL(spmm_generic_kernel<true>, dim3(blocks_for(total)), dim3(256), 0, s, n,
+                           nrhs, rp, col, val, X, x_sk, x_si, Y, y_sj, y_si, alpha, beta);
+    else
+        hipLaunchKernelGGL(spmm_generic_kernel<false>, dim3(blocks_for(total)), dim3(256), 0, s, n,
+                           nrhs, rp, col, val, X, x_sk, x_si, Y, y_sj, y_si, alpha, beta);
+    return hipGetLastError();
+}
+
+hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
+                                const float *val, const float *X, int64_t ldx, float *Y,
+                                int64_t ldy, float alpha, float beta, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int G = 1;
+    while (4 * G < nrhs) G <<= 1;
+    const unsigned grid = blocks_for((int64_t)n * G);
+#define SM_PANEL(GG)                                                                         \
+    case GG:                                                                                 \
+        hipLaunchKernelGGL(spmm_rowpanel_kernel<GG>, dim3(grid), dim3(256), 0, s, n, nrhs, rp, \
+                           col, val, X, ldx, Y, ldy, alpha, beta);                            \
+        break;
+    switch (G) {
+        SM_PANEL(1) SM_PANEL(2) SM_PANEL(4) SM_PANEL(8) SM_PANEL(16) SM_PANEL(32)
+        default: return hipErrorInvalidValue;
+    }
+#undef SM_PANEL
+    return hipGetLastError();
+}
+
+hipError_t launch_beta(float *c, int32_t m, int32_t n, int64_t ldc, float beta, hipStream_t s) {
+    const int64_t total = (int64_t)m * n;
+    if (total <= 0) return hipSuccess;
+    const int64_t grid = std::min<int64_t>(blocks_for(total), 256 * 16);
+    hipLaunchKernelGGL(beta_kernel, dim3((unsigned)grid), dim3(256), 0, s, c, m, n, ldc, beta);
+    return hipGetLastError();
+}
+
+hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, float *sa,
+                            int64_t ldsa, hipStream_t s) {
+    if (m <= 0 || n <= 0) return hipSuccess;
+    const int32_t tm = (m + 63) / 64, tn = (n + 63) / 64;
+    hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((int64_t)tm * tn)), dim3(256), 0, s, a, m,
+                       n, lda, sa, ldsa, tn);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
+                           const int32_t *col, int32_t *d_flag, hipStream_t s) {
+    hipLaunchKernelGGL(validate_kernel, dim3(blocks_for((int64_t)n_rows + 1)), dim3(256), 0, s,
+                       n_rows, n_cols, nnz, rp, col, d_flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_dense(int32_t n, const int32_t *rp, const int32_t *col,
+                                const float *val, float *out, int64_t stride, bool b_layout,
+                                hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_dense_kernel, dim3(blocks_for(n)), dim3(256), 0, s, n, rp, col, val,
+                       out, stride, b_layout);
+    return hipGetLastError();
+}
+
+}  // namespace smamd

@@ -1,0 +1,102 @@
+// sm_internal.h -- internal types shared by the C-ABI host code and the HIP
+// kernels of libsparsematrix_amd.so.  Not installed; the public surface is
+// include/sparsematrix.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "sparsematrix.h"
+
+namespace smamd {
+
+// ---- stream-kernel geometry (see DESIGN.md "Kernels") ----------------------
+constexpr int kStreamThreads = 256;       // 4 wavefronts per workgroup
+constexpr int kTileNnz = 4096;            // terms staged in LDS per row tile (16 KiB)
+constexpr int kTileRows = 1024;           // row cap per tile (empty-row heavy graphs)
+constexpr int kLongChunk = 4096;          // terms per workgroup for rows > kTileNnz
+constexpr int kSerialRowMax = SM_SERIAL_ROW_MAX;  // rows summed in reference order
+constexpr int kPadElems = 64;             // zero tail on col/val for aligned x4 loads
+
+// Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
+// holds a row longer than kSerialRowMax (wave-parallel reduction pass needed).
+struct alignas(16) Tile {
+    int32_t r0, r1, flags, pad;
+};
+
+// Chunk of a long row: terms [begin, end) of long row `lr` (index into
+// long_rows).  Partial sums are combined in chunk order by the finalize kernel.
+struct alignas(16) Chunk {
+    int32_t lr, begin, end, pad;
+};
+
+struct Plan {
+    int32_t n_tiles = 0;
+    Tile *d_tiles = nullptr;
+    int32_t n_long = 0;
+    int32_t *d_long_rows = nullptr;   // n_long
+    int32_t *d_long_ptr = nullptr;    // n_long + 1 offsets into chunks
+    int32_t n_chunks = 0;
+    Chunk *d_chunks = nullptr;
+    int32_t max_row_nnz = 0;
+    double avg_row_nnz = 0.0;
+};
+
+// Host launchers (kernels.hip).  All return hipError_t of the launch.
+hipError_t launch_spmv_parity(int32_t n, const int32_t *rp, const int32_t *col, const float *val,
+                              const float *x, float *y, float alpha, float beta, hipStream_t s);
+hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *col,
+                              const float *val, const float *x, float *y, float alpha,
+                              float beta, float *partials, hipStream_t s);
+hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
+                              const float *val, const float *x, float *y, float alpha, float beta,
+                              hipStream_t s);
+// Y(j, i) = beta*Y + alpha * sum_e B[j][e] * X(col_e, i), strides given per index.
+hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
+                               const float *val, const float *X, int64_t x_sk, int64_t x_si,
+                               float *Y, int64_t y_sj, int64_t y_si, float alpha, float beta,
+                               bool rhs_fastest, hipStream_t s);
+// Row-major X (k x nrhs, ldx) / Y (n x nrhs, ldy), nrhs % 4 == 0, 16-byte aligned.
+hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
+                                const float *val, const float *X, int64_t ldx, float *Y,
+                                int64_t ldy, float alpha, float beta, hipStream_t s);
+hipError_t launch_beta(float *c, int32_t m, int32_t n, int64_t ldc, float beta, hipStream_t s);
+hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, float *sa,
+                            int64_t ldsa, hipStream_t s);
+hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
+                           const int32_t *col, int32_t *d_flag, hipStream_t s);
+// Dense decode: out is zeroed by the caller.  b_layout: out[row*stride+col]
+// (B = S^T, CopyTo Trans); else out[col*stride+row] (S, CopyTo NoTrans).
+hipError_t launch_scatter_dense(int32_t n, const int32_t *rp, const int32_t *col,
+                                const float *val, float *out, int64_t stride, bool b_layout,
+                                hipStream_t s);
+hipError_t launch_panel_kernel(int variant, int32_t m, int32_t n, int32_t k, const float *a,
+                               int32_t lda, float *c, int32_t ldc, float alpha,
+                               const uint8_t *ppos, const uint8_t *pval, int32_t pos_len,
+                               const float *table, int32_t valid_table_size, void *workspace,
+                               hipStream_t s);
+size_t panel_kernel_workspace_bytes(int32_t pos_len, int32_t n);
+
+}  // namespace smamd
+
+// The opaque handle.
+struct sm_matrix {
+    int32_t device = 0;
+    int64_t n_rows = 0, n_cols = 0, nnz = 0;   // CSR of B = S^T
+    int64_t s_rows = 0, s_cols = 0;            // reference S view
+    int32_t *d_row_ptr = nullptr;
+    int32_t *d_col = nullptr;
+    float *d_val = nullptr;
+    smamd::Plan plan;
+    int64_t device_bytes = 0;
+    // Reference encoding (only for matrices built by sm_create_from_dense_index).
+    bool has_ref = false;
+    int32_t table_size = 0;
+    std::vector<float> table;                  // table_size + 1, last = 0
+    std::vector<uint8_t> pos, val;
+    std::vector<int32_t> panel_row_off, panel_col_off;
+    std::vector<int64_t> panel_begin, panel_end;
+};

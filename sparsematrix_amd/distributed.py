@@ -1,0 +1,45 @@
+"""Row-partitioned multi-GPU SpMV: one process per GPU, one all-gather of x.
+
+SURVEY.md §8(e): the rows of B (the outputs) are split into p equal contiguous
+slices, one per rank; every rank keeps global column indices; x is split the
+same way.  Per product the only exchange is one all-gather of x (RCCL over
+xGMI via torch.distributed's "nccl" backend, or gloo on CPU for tests),
+followed by the local SpMV into the rank's slice of y.  No other collective.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable
+
+
+@dataclass(frozen=True)
+class RowPartition:
+    n_rows: int
+    world: int
+
+    def bounds(self, rank: int) -> tuple[int, int]:
+        """[r0, r1) of `rank`: equal slices, the first n_rows % world ranks one row longer."""
+        q, r = divmod(self.n_rows, self.world)
+        r0 = rank * q + min(rank, r)
+        return r0, r0 + q + (1 if rank < r else 0)
+
+    def equal(self) -> bool:
+        """all_gather_into_tensor needs equal counts per rank."""
+        return self.n_rows % self.world == 0
+
+
+def slice_csr(row_ptr, col_idx, val, r0: int, r1: int):
+    """Rows [r0, r1) of a CSR (numpy or torch); columns stay global."""
+    a, b = int(row_ptr[r0]), int(row_ptr[r1])
+    rp = row_ptr[r0:r1 + 1] - row_ptr[r0]
+    return rp, col_idx[a:b], val[a:b]
+
+
+def allgather_spmv(local_spmv: Callable, x_local, x_full, y_local, group=None):
+    """x_full <- all_gather(x_local); y_local <- local_spmv(x_full, y_local).
+
+    `local_spmv(x_full, y_local)` is the rank's product (the HIP kernel through
+    the C ABI on GPU ranks)."""
+    import torch.distributed as dist
+    dist.all_gather_into_tensor(x_full, x_local, group=group)
+    return local_spmv(x_full, y_local)

@@ -1,0 +1,75 @@
+"""Shared helpers for the -m gpu parity tests (device buffers via torch)."""
+from __future__ import annotations
+
+import numpy as np
+
+TOL = 1e-6   # north_star: "within 1e-6 relative" -- defined against sum |terms|
+
+
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU test run without a visible GPU"
+    return torch
+
+
+def to_dev(a: np.ndarray):
+    torch = torch_dev()
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def to_host(t) -> np.ndarray:
+    torch = torch_dev()
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def assert_terms_close(got: np.ndarray, want: np.ndarray, absum: np.ndarray, tol: float = TOL):
+    """|got - want| <= tol * sum|terms| elementwise (and NaN where want is NaN)."""
+    got = np.asarray(got, np.float64).reshape(-1)
+    want = np.asarray(want, np.float64).reshape(-1)
+    absum = np.asarray(absum, np.float64).reshape(-1)
+    nan_w = np.isnan(want)
+    assert np.array_equal(nan_w, np.isnan(got)), "NaN pattern differs"
+    ok = ~nan_w
+    err = np.abs(got[ok] - want[ok])
+    bound = tol * absum[ok] + 1e-37
+    bad = err > bound
+    assert not bad.any(), (f"{int(bad.sum())} elements out of bound; worst ratio "
+                           f"{float((err / bound).max()):.3g}")
+
+
+def bits(a) -> np.ndarray:
+    return np.ascontiguousarray(a, np.float32).reshape(-1).view(np.uint32)
+
+
+def uniform_csr(n_rows: int, n_cols: int, per_row: int, seed: int, table=None):
+    """`per_row` distinct sorted columns per row, values from a 255-entry table."""
+    rng = np.random.default_rng(seed)
+    cols = np.sort(rng.integers(0, n_cols, (n_rows, per_row), dtype=np.int64), axis=1)
+    # make columns distinct within a row: bump duplicates forward, then re-sort
+    for _ in range(8):
+        dup = np.zeros_like(cols, bool)
+        dup[:, 1:] = cols[:, 1:] == cols[:, :-1]
+        if not dup.any():
+            break
+        cols[dup] = rng.integers(0, n_cols, int(dup.sum()))
+        cols.sort(axis=1)
+    if table is None:
+        table = rng.uniform(-1, 1, 255).astype(np.float32)
+    val = table[rng.integers(0, 255, n_rows * per_row)].astype(np.float32)
+    rp = np.arange(0, n_rows * per_row + 1, per_row, dtype=np.int32)
+    return rp, cols.reshape(-1).astype(np.int32), val
+
+
+def skewed_csr(n_rows: int, n_cols: int, lengths: np.ndarray, seed: int):
+    """CSR with the given row lengths (unsorted columns allowed to repeat)."""
+    rng = np.random.default_rng(seed)
+    lengths = np.asarray(lengths, np.int64)
+    rp = np.zeros(n_rows + 1, np.int64)
+    rp[1:] = np.cumsum(lengths)
+    nnz = int(rp[-1])
+    col = np.empty(nnz, np.int32)
+    for r in range(n_rows):
+        col[rp[r]:rp[r + 1]] = np.sort(rng.integers(0, n_cols, int(lengths[r])))
+    val = rng.uniform(-1, 1, nnz).astype(np.float32)
+    return rp.astype(np.int32), col, val

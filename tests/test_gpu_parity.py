@@ -1,0 +1,341 @@
+"""Parity of the HIP path (through the C ABI) with the reference.
+
+Bit-exact against the reference's own outputs (tests/golden) for the encoding,
+CopyTo and AddMatMat; bit-exact against the oracle for the parity kernels and
+for every fast-kernel row of <= SM_SERIAL_ROW_MAX terms; |err| <= 1e-6 sum|terms|
+for longer rows.  Full BASELINE sizes are checked through size-independent
+properties (stream == parity bit-for-bit on 16-term rows, linearity).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from golden_util import bits_equal, case_names, load_case
+from gpu_util import (assert_terms_close, bits, skewed_csr, to_dev, to_host, torch_dev,
+                      uniform_csr)
+
+pytestmark = pytest.mark.gpu
+
+SERIAL_MAX = 64
+
+
+@pytest.fixture(scope="module")
+def sm():
+    torch_dev()
+    oracle.build()
+    import sparsematrix_amd
+    sparsematrix_amd.load()
+    return sparsematrix_amd
+
+
+def _from_case(sm, c):
+    return sm.SparseMatrix(c.dm, c.rows, c.cols, c.stride, c.table, c.table_size,
+                           sm.SblasTrans if c.trans else sm.SblasNoTrans)
+
+
+# ---------------------------------------------------------------------------- golden
+@pytest.mark.parametrize("name", case_names())
+def test_golden_encoding_and_copyto(sm, name):
+    c = load_case(name)
+    M = _from_case(sm, c)
+    assert (M.NumRows(), M.NumCols()) == (c.s_rows, c.s_cols)
+    st = M.ref_stream()
+    assert np.array_equal(st["pos"], c.pos) and np.array_equal(st["val"], c.val)
+    assert np.array_equal(st["panel_col_off"], c.panel_col_off)
+    assert np.array_equal(st["panel_begin"], c.panel_begin)
+    assert np.array_equal(st["panel_end"], c.panel_end)
+    for tr, (stride, want) in c.copyto.items():
+        out = np.full(want.size, np.nan, np.float32)
+        M.CopyTo(out, stride, tr)
+        assert bits_equal(out, want)
+    got = M.CopyTo(None, c.s_rows, sm.SblasTrans)[: c.s_cols * c.s_rows]
+    assert bits_equal(got.reshape(c.s_cols, c.s_rows), c.dense_b())
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_addmatmat_host_bit_exact(sm, name):
+    """The drop-in AddMatMat on host pointers is bit-identical to the reference."""
+    c = load_case(name)
+    M = _from_case(sm, c)
+    for r in c.runs:
+        out = r.c.copy()
+        M.AddMatMat(r.a, r.m, r.lda, out, r.ldc, r.alpha, r.beta)
+        assert bits_equal(out, r.out), (r.m, r.alpha, r.beta)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_addmatmat_device(sm, name):
+    c = load_case(name)
+    M = _from_case(sm, c)
+    rp, ci, va = M.csr()
+    max_row = int(np.diff(rp).max()) if rp.size > 1 else 0
+    for r in c.runs:
+        for algo in ("parity", "auto"):
+            a_d, c_d = to_dev(r.a), to_dev(r.c)
+            M.AddMatMat(a_d, r.m, r.lda, c_d, r.ldc, r.alpha, r.beta, algo=algo)
+            got = to_host(c_d)
+            if algo == "parity" or max_row <= SERIAL_MAX:
+                assert bits_equal(got, r.out), (algo, r.m, r.alpha, r.beta)
+            else:
+                # tree-summed long rows: compare each output row against the oracle bound
+                A = r.a.reshape(r.m, r.lda)
+                Cin = r.c.reshape(r.m, r.ldc)
+                for i in range(r.m):
+                    y64, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, A[i, : c.s_rows],
+                                                  Cin[i, : c.s_cols], r.alpha, r.beta)
+                    assert_terms_close(got.reshape(r.m, r.ldc)[i, : c.s_cols],
+                                       r.out.reshape(r.m, r.ldc)[i, : c.s_cols], ab)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_spmv_spmm_all_algos(sm, name):
+    """CSR SpMV / SpMM on the golden matrices vs the reference's AddMatMat outputs."""
+    c = load_case(name)
+    M = _from_case(sm, c)
+    rp, ci, va = M.csr()
+    k, n = c.s_rows, c.s_cols
+    max_row = int(np.diff(rp).max()) if rp.size > 1 else 0
+    for r in c.runs:
+        A = r.a.reshape(r.m, r.lda)[:, :k]
+        Cin = r.c.reshape(r.m, r.ldc)[:, :n]
+        want = r.out.reshape(r.m, r.ldc)[:, :n]
+        for algo in ("parity", "stream", "vector", "auto"):
+            y = to_dev(Cin[0].copy())
+            M.spmv(to_dev(A[0].copy()), y, r.alpha, r.beta, algo=algo)
+            got = to_host(y)
+            if algo == "parity" or (algo in ("stream", "auto") and max_row <= SERIAL_MAX):
+                assert bits_equal(got, want[0]), algo
+            else:
+                _, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, A[0], Cin[0], r.alpha,
+                                            r.beta)
+                assert_terms_close(got, want[0], ab)
+        # SpMM, row-major X (k x m) / Y (n x m): every output element in stored order
+        for algo in ("auto", "parity"):
+            X = to_dev(np.ascontiguousarray(A.T))
+            Y = to_dev(np.ascontiguousarray(Cin.T))
+            M.spmm(X, Y, r.alpha, r.beta, algo=algo)
+            assert bits_equal(to_host(Y).T, want), (algo, r.m)
+
+
+# ---------------------------------------------------------------------------- oracle, larger
+@pytest.mark.parametrize("n_rows,n_cols,per_row", [(65536, 65536, 16), (4099, 70000, 3),
+                                                   (3001, 1 << 20, 64), (1000, 5000, 65)])
+def test_uniform_rows_vs_oracle(sm, n_rows, n_cols, per_row):
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (-2.0, 0.0)):
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        _, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, x, y0, alpha, beta)
+        for algo in ("parity", "stream", "vector"):
+            y = to_dev(y0)
+            M.spmv(to_dev(x), y, alpha, beta, algo=algo)
+            got = to_host(y)
+            if algo == "parity" or (algo == "stream" and per_row <= SERIAL_MAX):
+                assert np.array_equal(bits(got), bits(want)), algo
+            else:
+                assert_terms_close(got, want, ab)
+
+
+def test_skewed_rows_long_row_split(sm):
+    """Power-law-like lengths incl. rows > 4096 terms (split across workgroups),
+    rows in (64, 4096] (wave reduction), empty rows and unaligned tile starts."""
+    rng = np.random.default_rng(3)
+    n_rows, n_cols = 20000, 300000
+    lengths = np.minimum(rng.zipf(1.6, n_rows), 30000)
+    lengths[::97] = 0
+    lengths[5] = 50001
+    lengths[6] = 4097
+    lengths[7] = 4096
+    lengths[8] = 65
+    rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=4)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    info = M.info()
+    assert info["n_long_rows"] >= 2 and info["max_row_nnz"] == 50001
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y0, 1.3, 0.7)
+    _, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, x, y0, 1.3, 0.7)
+    short = np.diff(rp) <= SERIAL_MAX
+    for algo in ("parity", "stream", "vector", "auto"):
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, 1.3, 0.7, algo=algo)
+        got = to_host(y)
+        if algo == "parity":
+            assert np.array_equal(bits(got), bits(want))
+        else:
+            assert_terms_close(got, want, ab)
+            if algo in ("stream", "auto"):
+                assert np.array_equal(bits(got[short]), bits(want[short]))
+
+
+def test_spmm_n32_vs_oracle(sm):
+    n_rows, n_cols, N = 30000, 40000, 32
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=11)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    rng = np.random.default_rng(12)
+    X = rng.uniform(-1, 1, (n_cols, N)).astype(np.float32)
+    Y0 = rng.uniform(-1, 1, (n_rows, N)).astype(np.float32)
+    want = oracle.csr_spmm(rp.astype(np.int64), ci, va, X, Y0, 1.3, 0.7)
+    for algo in ("auto", "parity"):
+        Y = to_dev(Y0)
+        M.spmm(to_dev(X), Y, 1.3, 0.7, algo=algo)
+        assert np.array_equal(bits(to_host(Y)), bits(want)), algo
+    # odd N and padded leading dimensions take the generic kernel
+    torch = torch_dev()
+    for N2 in (1, 3, 12, 33):
+        Xp = torch.zeros((n_cols, N2 + 5), dtype=torch.float32, device="cuda")
+        Xp[:, :N2] = to_dev(X[:, :N2].copy())
+        Yp = torch.zeros((n_rows, N2 + 3), dtype=torch.float32, device="cuda")
+        Yp[:, :N2] = to_dev(Y0[:, :N2].copy())
+        M.spmm(Xp[:, :N2], Yp[:, :N2], 1.3, 0.7)
+        want2 = oracle.csr_spmm(rp.astype(np.int64), ci, va, X[:, :N2].copy(),
+                                Y0[:, :N2].copy(), 1.3, 0.7)
+        assert np.array_equal(bits(to_host(Yp)[:, :N2]), bits(want2)), N2
+
+
+# ---------------------------------------------------------------------------- edge cases
+def test_semantics_alpha_zero_beta_zero_nan(sm):
+    rp, ci, va = uniform_csr(1000, 1000, 5, seed=1)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, 1000)
+    x = np.full(1000, np.nan, np.float32)             # alpha == 0 never touches x
+    y0 = np.arange(1000, dtype=np.float32)
+    for algo in ("parity", "stream", "vector"):
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, 0.0, 2.0, algo=algo)
+        assert np.array_equal(to_host(y), y0 * 2)
+    y0n = y0.copy()
+    y0n[::3] = np.nan                                   # beta == 0 propagates NaN in y
+    x = np.ones(1000, np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y0n, 1.0, 0.0)
+    assert np.isnan(want[::3]).all()
+    for algo in ("parity", "stream", "vector"):
+        y = to_dev(y0n)
+        M.spmv(to_dev(x), y, 1.0, 0.0, algo=algo)
+        got = to_host(y)
+        assert np.array_equal(np.isnan(got), np.isnan(want))
+
+
+def test_empty_and_degenerate(sm):
+    # val_table_size == 0 -> empty 0 x 0 matrix (sparse-matrix.cc:26)
+    E = sm.SparseMatrix(np.zeros(4, np.uint8), 2, 2, 2, np.zeros(1, np.float32), 0)
+    assert (E.NumRows(), E.NumCols()) == (0, 0)
+    # all-empty rows
+    rp = np.zeros(11, np.int32)
+    M = sm.SparseMatrix.from_csr(rp, np.zeros(0, np.int32), np.zeros(0, np.float32), 7)
+    y = to_dev(np.arange(10, dtype=np.float32))
+    M.spmv(to_dev(np.ones(7, np.float32)), y, 1.0, 0.5)
+    assert np.array_equal(to_host(y), np.arange(10, dtype=np.float32) * 0.5)
+    # zero rows
+    Z = sm.SparseMatrix.from_csr(np.zeros(1, np.int32), np.zeros(0, np.int32),
+                                 np.zeros(0, np.float32), 5)
+    assert Z.info()["n_rows"] == 0
+    # one giant row: three chunks
+    rp, ci, va = skewed_csr(1, 1 << 16, np.array([12000]), seed=9)
+    G = sm.SparseMatrix.from_csr(rp, ci, va, 1 << 16)
+    x = np.random.default_rng(0).uniform(-1, 1, 1 << 16).astype(np.float32)
+    y0 = np.array([0.25], np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 1.0)
+    _, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, x, y0, 1.0, 1.0)
+    y = to_dev(y0)
+    G.spmv(to_dev(x), y)
+    assert_terms_close(to_host(y), want, ab)
+
+
+def test_invalid_csr_rejected(sm):
+    torch = torch_dev()
+    rp = torch.tensor([0, 2, 3], dtype=torch.int32, device="cuda")
+    ci = torch.tensor([0, 9, 1], dtype=torch.int32, device="cuda")   # 9 >= n_cols
+    va = torch.ones(3, dtype=torch.float32, device="cuda")
+    with pytest.raises(sm.SparseMatrixError) as ei:
+        sm.SparseMatrix.from_csr(rp, ci, va, 4)
+    assert ei.value.status == 6
+    with pytest.raises(sm.SparseMatrixError):
+        sm.SparseMatrix.from_csr(np.array([0, 2, 1], np.int32), np.zeros(2, np.int32),
+                                 np.zeros(2, np.float32), 4)
+
+
+def test_device_csr_ingestion_matches_host(sm):
+    rp, ci, va = uniform_csr(5000, 9000, 7, seed=21)
+    A = sm.SparseMatrix.from_csr(rp, ci, va, 9000)
+    B = sm.SparseMatrix.from_csr(to_dev(rp), to_dev(ci), to_dev(va), 9000)
+    assert A == B
+    assert A.info()["n_tiles"] == B.info()["n_tiles"]
+
+
+def test_equality_semantics(sm):
+    c = load_case("sweep_255x257_0.001_t_T255") if "sweep_255x257_0.001_t_T255" in case_names() \
+        else load_case(case_names()[0])
+    A, B = _from_case(sm, c), _from_case(sm, c)
+    assert A == B
+    d = c.dm.copy()
+    idx = np.flatnonzero(d.reshape(c.rows, c.stride)[:, : c.cols].reshape(-1) < 255)
+    if idx.size:
+        d2 = d.reshape(c.rows, c.stride)
+        i = idx[0]
+        d2[i // c.cols, i % c.cols] = 255
+        C = sm.SparseMatrix(d2.reshape(-1), c.rows, c.cols, c.stride, c.table, c.table_size,
+                            sm.SblasTrans if c.trans else sm.SblasNoTrans)
+        assert not (A == C)
+
+
+def test_selftest(sm):
+    assert sm.SparseMatrix.SelfTest()
+
+
+def test_kernel_helpers(sm):
+    torch = torch_dev()
+    rng = np.random.default_rng(5)
+    m, n, lda, ldsa = 1023, 511, 512, 1024        # kernel_test.cc:33
+    a = rng.uniform(-1000, 1000, 1024 * 512).astype(np.float32)
+    sa = torch.zeros(n * ldsa, dtype=torch.float32, device="cuda")
+    sm.sblas_trans_kernel(to_dev(a), m, n, lda, sa, ldsa)
+    want = a.reshape(1024, 512)[:m, :n].T
+    assert np.array_equal(to_host(sa).reshape(n, ldsa)[:, :m], want)
+    c = rng.uniform(-1000, 1000, 37 * 41).astype(np.float32)
+    cd = to_dev(c)
+    sm.sblas_beta_operation_kernel(cd, 37, 39, 41, 0.7)
+    assert bits_equal(to_host(cd), oracle.beta_scale(c, 37, 39, 41, 0.7))
+
+
+# ---------------------------------------------------------------------------- full size
+@pytest.mark.slow
+def test_full_size_config2_properties(sm):
+    """BASELINE config 2 (2^20 x 2^20, 16 terms/row): stream == parity bit-for-bit,
+    linearity in x, and a sample of rows against the oracle."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x1 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    x2 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    yp, ys = y0.clone(), y0.clone()
+    M.spmv(x1, yp, 1.0, 0.5, algo="parity")
+    M.spmv(x1, ys, 1.0, 0.5, algo="stream")
+    torch.cuda.synchronize()
+    assert torch.equal(yp.view(torch.int32), ys.view(torch.int32))
+    # linearity: B(x1 + x2) ~= B x1 + B x2 within 1e-6 * sum|terms| (abs values)
+    z = torch.zeros(n, device="cuda")
+    y12, y1, y2, yabs = z.clone(), z.clone(), z.clone(), z.clone()
+    M.spmv(x1 + x2, y12, 1.0, 0.0)
+    M.spmv(x1, y1, 1.0, 0.0)
+    M.spmv(x2, y2, 1.0, 0.0)
+    Mabs = sm.SparseMatrix.from_csr(rp, ci, va.abs(), n)
+    Mabs.spmv(x1.abs() + x2.abs(), yabs, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert bool(((y12 - (y1 + y2)).abs() <= 4e-6 * yabs + 1e-30).all())
+    # sampled rows vs the oracle
+    rows = np.random.default_rng(0).choice(n, 2000, replace=False)
+    rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+    x1h, y0h = x1.cpu().numpy(), y0.cpu().numpy()
+    sub_rp = np.zeros(rows.size + 1, np.int64)
+    sub_rp[1:] = np.cumsum(rph[rows + 1] - rph[rows])
+    sub_ci = np.concatenate([cih[rph[r]:rph[r + 1]] for r in rows])
+    sub_va = np.concatenate([vah[rph[r]:rph[r + 1]] for r in rows])
+    want = oracle.csr_spmv(sub_rp, sub_ci, sub_va, x1h, y0h[rows], 1.0, 0.5)
+    assert np.array_equal(bits(ys.cpu().numpy()[rows]), bits(want))
