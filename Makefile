@@ -15,7 +15,27 @@ OBJS      = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
             $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS      = include/sparsematrix.h $(wildcard $(CSRC)/*.h)
 
-all: $(LIB) oracle
+all: $(LIB) $(SHIM) oracle compat
+
+# C++ drop-in shim (reference class/kernel signatures) over the C ABI
+$(SHIM): $(CSRC)/sblas_shim.cpp include/sblas/sparse-matrix.h include/sblas/kernel.h $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -shared -Iinclude/sblas -Iinclude \
+	    -o $@ $(CSRC)/sblas_shim.cpp -L$(PKG) -lsparsematrix_amd -Wl,-rpath,'$$ORIGIN'
+
+# The reference's own unit tests (src/sparse/kernel_test.cc, sparse-matrix_test.cc),
+# compiled UNCHANGED from /root/reference against include/sblas + libsblas.so.
+# Only where /root/reference exists (the binaries travel to the GPU box).
+REFSRC ?= /root/reference/src/sparse
+COMPAT  = build/compat/kernel_test build/compat/sparse-matrix_test
+ifneq ($(wildcard $(REFSRC)/kernel_test.cc),)
+compat: $(COMPAT)
+build/compat/%: $(REFSRC)/%.cc $(SHIM)
+	@mkdir -p build/compat
+	g++ -std=c++11 -O2 -w -Iinclude/sblas -o $@ $< -L$(PKG) -lsblas -lsparsematrix_amd \
+	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+else
+compat:
+endif
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -35,4 +55,4 @@ clean:
 	rm -rf build $(LIB) $(SHIM)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean compat

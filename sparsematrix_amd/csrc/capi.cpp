@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -80,9 +81,19 @@ void free_device(sm_matrix *m) {
 }
 
 // Build the stream plan from a host row_ptr and upload it.
+// Tile size: kTileNnz unless SM_TILE_NNZ (1024/2048/4096/8192) overrides it
+// (tuning knob, read at matrix creation).
+int32_t tile_nnz_setting() {
+    const char *e = getenv("SM_TILE_NNZ");
+    if (!e) return kTileNnz;
+    const int v = atoi(e);
+    return (v == 1024 || v == 2048 || v == 4096 || v == 8192) ? v : kTileNnz;
+}
+
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
-    plan_rows(rp_host, m->n_rows, kTileNnz, kTileRows, kLongChunk, kSerialRowMax, ph);
+    const int32_t tile = tile_nnz_setting();
+    plan_rows(rp_host, m->n_rows, tile, kTileRows, kLongChunk, kSerialRowMax, ph);
     std::vector<Tile> tiles(ph.tiles.size());
     for (size_t i = 0; i < tiles.size(); i++)
         tiles[i] = Tile{ph.tiles[i].r0, ph.tiles[i].r1, ph.tiles[i].flags, 0};
@@ -90,6 +101,7 @@ sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     for (size_t i = 0; i < chunks.size(); i++)
         chunks[i] = Chunk{ph.chunks[i].lr, ph.chunks[i].begin, ph.chunks[i].end, 0};
     Plan &p = m->plan;
+    p.tile_nnz = tile;
     p.n_tiles = (int32_t)tiles.size();
     p.n_long = (int32_t)ph.long_rows.size();
     p.n_chunks = (int32_t)chunks.size();
@@ -583,10 +595,25 @@ sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t k, cons
                           int32_t lda, float *c, int32_t ldc, float alpha, const uint8_t *ppos,
                           const uint8_t *pval, int32_t pos_len, const float *table,
                           int32_t valid_table_size, sm_stream stream) {
-    (void)variant; (void)m; (void)n; (void)k; (void)a; (void)lda; (void)c; (void)ldc;
-    (void)alpha; (void)ppos; (void)pval; (void)pos_len; (void)table; (void)valid_table_size;
-    (void)stream;
-    return fail(SM_ERR_NOT_SUPPORTED, "sm_panel_kernel: reference-format kernels not built yet");
+    if (variant < 0 || variant > 3) return fail(SM_ERR_INVALID_ARG, "variant must be 0..3");
+    if (m < 0 || n < 0 || k < 0 || n > 256 || pos_len < 0)
+        return fail(SM_ERR_INVALID_ARG, "bad panel shape m=%d n=%d k=%d pos_len=%d", m, n, k, pos_len);
+    if (valid_table_size < 0 || valid_table_size > 255)
+        return fail(SM_ERR_INVALID_ARG, "valid_table_size not in [0, 255]");
+    const bool tr = variant >= 2;
+    if (m > 0 && ((!tr && (lda < k || ldc < n)) || (tr && (lda < m || ldc < m))))
+        return fail(SM_ERR_INVALID_ARG, "lda/ldc too small for variant %d", variant);
+    if ((int64_t)m * n == 0 || pos_len == 0) return SM_OK;
+    if (!a || !c || !ppos || !pval || !table) return fail(SM_ERR_INVALID_ARG, "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    void *ws = nullptr;
+    hipError_t e = hipMallocAsync(&ws, panel_kernel_workspace_bytes(pos_len, n), s);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(panel workspace)");
+    e = launch_panel_kernel(variant, m, n, k, a, lda, c, ldc, alpha, ppos, pval, pos_len, table,
+                            valid_table_size, ws, s);
+    hipError_t e2 = hipFreeAsync(ws, s);
+    if (e == hipSuccess) e = e2;
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_panel_kernel");
 }
 
 sm_status sm_stream_sync(sm_stream stream) {

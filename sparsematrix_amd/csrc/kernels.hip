@@ -93,6 +93,7 @@ __global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
     float alpha, float beta, float *__restrict__ partials) {
     constexpr int kLds = TILE + TILE / 32 + 8;
     constexpr int kWaves = THREADS / 64;
+    constexpr int kIt = TILE / (4 * THREADS) + 1;   // +1: unaligned tile start
     __shared__ float prod[kLds];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -103,13 +104,32 @@ __global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
         // ---- one chunk of a long row: tree sum of its terms ----------------
         const Chunk ch = chunks[b];
         float s = 0.0f;
-        for (int32_t i = (ch.begin & ~3) + 4 * tid; i < ch.end; i += 4 * THREADS) {
-            const float4 v = ld_stream(reinterpret_cast<const float4 *>(val + i));
-            const int4 c = ld_stream(reinterpret_cast<const int4 *>(col + i));
-            if (i + 0 >= ch.begin && i + 0 < ch.end) s = add_rn(s, term(x[c.x], v.x, alpha));
-            if (i + 1 >= ch.begin && i + 1 < ch.end) s = add_rn(s, term(x[c.y], v.y, alpha));
-            if (i + 2 >= ch.begin && i + 2 < ch.end) s = add_rn(s, term(x[c.z], v.z, alpha));
-            if (i + 3 >= ch.begin && i + 3 < ch.end) s = add_rn(s, term(x[c.w], v.w, alpha));
+        for (int32_t i0 = (ch.begin & ~3) + 4 * tid; i0 < ch.end; i0 += 4 * THREADS * kIt) {
+            float4 vv[kIt];
+            int4 cc[kIt];
+#pragma unroll
+            for (int it = 0; it < kIt; ++it) {
+                const int32_t i = i0 + 4 * THREADS * it;
+                const int32_t il = i < ch.end ? i : i0;
+                vv[it] = ld_stream(reinterpret_cast<const float4 *>(val + il));
+                cc[it] = ld_stream(reinterpret_cast<const int4 *>(col + il));
+            }
+            float xg[kIt][4];
+#pragma unroll
+            for (int it = 0; it < kIt; ++it) {
+                xg[it][0] = x[cc[it].x]; xg[it][1] = x[cc[it].y];
+                xg[it][2] = x[cc[it].z]; xg[it][3] = x[cc[it].w];
+            }
+#pragma unroll
+            for (int it = 0; it < kIt; ++it) {
+                const int32_t i = i0 + 4 * THREADS * it;
+                const float vq[4] = {vv[it].x, vv[it].y, vv[it].z, vv[it].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float tq = term(xg[it][q], vq[q], alpha);
+                    if (i + q >= ch.begin && i + q < ch.end) s = add_rn(s, tq);
+                }
+            }
         }
         s = wave_sum(s);
         if (lane == 0) prod[wave] = s;
@@ -127,35 +147,63 @@ __global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
     const Tile t = tiles[b - n_chunks];
     const int32_t s0 = rp[t.r0];
     const int32_t e0 = rp[t.r1];
-    const int32_t base = s0 & ~3;
-    constexpr int kIt = TILE / (4 * THREADS) + 1;   // +1: unaligned tile start
-    float4 vv[kIt];
-    int4 cc[kIt];
-#pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const int32_t i = base + 4 * (tid + it * THREADS);
-        if (i < e0) {
-            vv[it] = ld_stream(reinterpret_cast<const float4 *>(val + i));
-            cc[it] = ld_stream(reinterpret_cast<const int4 *>(col + i));
-        }
+    // Row bounds and y of this thread's first row, fetched before the tile's
+    // terms so their latency hides under the stream.
+    const int32_t r_first = t.r0 + tid;
+    const bool has_row = r_first < t.r1;
+    int32_t ra = 0, re = 0;
+    float y_first = 0.0f;
+    if (has_row) {
+        ra = rp[r_first];
+        re = rp[r_first + 1];
+        y_first = y[r_first];
     }
+    if (e0 > s0) {
+        // Aligned 16-byte loads over [s0 & ~3, e0): every slot loads (slots past
+        // the tile re-read the first vector), so the col/val loads and then all
+        // x gathers issue back to back with no branch between them.  Columns of
+        // slots outside [s0, e0) belong to neighbouring rows or to the zeroed
+        // pad: always valid indices.
+        const int32_t base = s0 & ~3;
+        float4 vv[kIt];
+        int4 cc[kIt];
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const int32_t i = base + 4 * (tid + it * THREADS);
-        if (i < e0) {
+        for (int it = 0; it < kIt; ++it) {
+            const int32_t i = base + 4 * (tid + it * THREADS);
+            const int32_t il = i < e0 ? i : base;
+            vv[it] = ld_stream(reinterpret_cast<const float4 *>(val + il));
+            cc[it] = ld_stream(reinterpret_cast<const int4 *>(col + il));
+        }
+        float xg[kIt][4];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            xg[it][0] = x[cc[it].x]; xg[it][1] = x[cc[it].y];
+            xg[it][2] = x[cc[it].z]; xg[it][3] = x[cc[it].w];
+        }
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const int32_t i = base + 4 * (tid + it * THREADS);
             const float vq[4] = {vv[it].x, vv[it].y, vv[it].z, vv[it].w};
-            const int32_t cq[4] = {cc[it].x, cc[it].y, cc[it].z, cc[it].w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int32_t idx = i + q;
-                if (idx >= s0 && idx < e0) prod[lds_slot(idx - s0)] = term(x[cq[q]], vq[q], alpha);
+                const float tq = term(xg[it][q], vq[q], alpha);
+                if (idx >= s0 && idx < e0) prod[lds_slot(idx - s0)] = tq;
             }
         }
     }
     __syncthreads();
 
     // Short rows: one thread each, terms in stored order (reference order).
-    for (int32_t r = t.r0 + tid; r < t.r1; r += THREADS) {
+    if (has_row && re - ra <= kSerialRowMax) {
+        float acc = y_first;
+        if (beta != 1.0f) acc = mul_rn(acc, beta);
+        const int32_t a = ra - s0, e = re - s0;
+#pragma unroll 4
+        for (int32_t k = a; k < e; ++k) acc = add_rn(acc, prod[lds_slot(k)]);
+        y[r_first] = acc;
+    }
+    for (int32_t r = r_first + THREADS; r < t.r1; r += THREADS) {
         const int32_t a = rp[r] - s0;
         const int32_t e = rp[r + 1] - s0;
         if (e - a > kSerialRowMax) continue;
@@ -371,9 +419,17 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               float beta, float *partials, hipStream_t s) {
     const int64_t grid = (int64_t)p.n_chunks + p.n_tiles;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, kTileNnz>), dim3((unsigned)grid),
-                       dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, col, val,
-                       x, y, alpha, beta, partials);
+#define SM_STREAM(TT)                                                                         \
+    case TT:                                                                                  \
+        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)grid),     \
+                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp,  \
+                           col, val, x, y, alpha, beta, partials);                            \
+        break;
+    switch (p.tile_nnz) {
+        SM_STREAM(1024) SM_STREAM(2048) SM_STREAM(4096) SM_STREAM(8192)
+        default: return hipErrorInvalidValue;
+    }
+#undef SM_STREAM
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.n_long == 0) return e;
     hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.n_long)), dim3(256), 0, s,

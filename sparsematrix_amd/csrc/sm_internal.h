@@ -15,7 +15,7 @@ namespace smamd {
 
 // ---- stream-kernel geometry (see DESIGN.md "Kernels") ----------------------
 constexpr int kStreamThreads = 256;       // 4 wavefronts per workgroup
-constexpr int kTileNnz = 4096;            // terms staged in LDS per row tile (16 KiB)
+constexpr int kTileNnz = 4096;            // default terms staged in LDS per row tile (16 KiB)
 constexpr int kTileRows = 1024;           // row cap per tile (empty-row heavy graphs)
 constexpr int kLongChunk = 4096;          // terms per workgroup for rows > kTileNnz
 constexpr int kSerialRowMax = SM_SERIAL_ROW_MAX;  // rows summed in reference order
@@ -34,6 +34,7 @@ struct alignas(16) Chunk {
 };
 
 struct Plan {
+    int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
     int32_t n_long = 0;

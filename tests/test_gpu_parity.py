@@ -185,14 +185,16 @@ def test_spmm_n32_vs_oracle(sm):
         assert np.array_equal(bits(to_host(Y)), bits(want)), algo
     # odd N and padded leading dimensions take the generic kernel
     torch = torch_dev()
+    XW = rng.uniform(-1, 1, (n_cols, 40)).astype(np.float32)
+    YW = rng.uniform(-1, 1, (n_rows, 40)).astype(np.float32)
     for N2 in (1, 3, 12, 33):
         Xp = torch.zeros((n_cols, N2 + 5), dtype=torch.float32, device="cuda")
-        Xp[:, :N2] = to_dev(X[:, :N2].copy())
+        Xp[:, :N2] = to_dev(XW[:, :N2].copy())
         Yp = torch.zeros((n_rows, N2 + 3), dtype=torch.float32, device="cuda")
-        Yp[:, :N2] = to_dev(Y0[:, :N2].copy())
+        Yp[:, :N2] = to_dev(YW[:, :N2].copy())
         M.spmm(Xp[:, :N2], Yp[:, :N2], 1.3, 0.7)
-        want2 = oracle.csr_spmm(rp.astype(np.int64), ci, va, X[:, :N2].copy(),
-                                Y0[:, :N2].copy(), 1.3, 0.7)
+        want2 = oracle.csr_spmm(rp.astype(np.int64), ci, va, XW[:, :N2].copy(),
+                                YW[:, :N2].copy(), 1.3, 0.7)
         assert np.array_equal(bits(to_host(Yp)[:, :N2]), bits(want2)), N2
 
 
@@ -339,3 +341,41 @@ def test_full_size_config2_properties(sm):
     sub_va = np.concatenate([vah[rph[r]:rph[r + 1]] for r in rows])
     want = oracle.csr_spmv(sub_rp, sub_ci, sub_va, x1h, y0h[rows], 1.0, 0.5)
     assert np.array_equal(bits(ys.cpu().numpy()[rows]), bits(want))
+
+
+# ---------------------------------------------------------------------------- drop-in surfaces
+def test_reference_unit_tests_compiled_against_shim(sm):
+    """The reference's own src/sparse/kernel_test.cc and sparse-matrix_test.cc, compiled
+    unchanged against include/sblas (Makefile `compat`), pass on the GPU."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bins = [os.path.join(root, "build", "compat", b) for b in ("kernel_test", "sparse-matrix_test")]
+    if not all(os.path.exists(b) for b in bins):
+        pytest.skip("compat binaries are built only where /root/reference exists")
+    for b in bins:
+        r = subprocess.run([b], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "success" in r.stdout, (b, r.stdout, r.stderr)
+
+
+def test_panel_kernels_vs_golden(sm):
+    """sm_panel_kernel (reference stream format on the device) vs the four exported
+    reference variants (kernel.cc:213-369, 771-800), bit-exact."""
+    import ctypes as C
+    from golden_util import load_kernels
+    from sparsematrix_amd import _lib
+    k = load_kernels()
+    L = _lib.load()
+    pos, val, tab = to_dev(k["pos"]), to_dev(k["val"]), to_dev(k["table"])
+    m, n, kk = int(k["m"]), int(k["n"]), int(k["k"])
+    alpha = float(k["alpha"])
+    for v in range(4):
+        if v < 2:
+            a, c, lda, ldc = to_dev(k["a"]), to_dev(k["c"]), int(k["lda"]), int(k["ldc"])
+        else:
+            a, c, lda, ldc = to_dev(k["aT"]), to_dev(k["cT"]), int(k["ldt"]), int(k["ldt"])
+        st = L.sm_panel_kernel(v, m, n, kk, a.data_ptr(), lda, c.data_ptr(), ldc, alpha,
+                               pos.data_ptr(), val.data_ptr(), int(k["pos"].size),
+                               tab.data_ptr(), int(k["table_size"]), None)
+        assert st == 0, L.sm_last_error()
+        assert bits_equal(to_host(c), k[f"out_v{v}"]), v
