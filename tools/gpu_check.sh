@@ -24,7 +24,7 @@ fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   rm -rf "$OUT/prof"
-  ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+  ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu ) > "$OUT/prof.log" 2>&1 || { tail -30 "$OUT/prof.log"; exit 14; }
   find "$OUT/prof" -name '*stats*' | head
 fi
