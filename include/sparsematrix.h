@@ -22,9 +22,10 @@
  *                                                        sparse-matrix.cc:44, 77
  * Summation order: SM_ALGO_PARITY adds the terms of every output in stored
  * (ascending column) order, exactly as the reference does, so results are
- * bit-identical to the reference CPU kernel.  SM_ALGO_AUTO/STREAM/SPMM keep
- * that order for rows of up to SM_SERIAL_ROW_MAX terms and use a tree sum for
- * longer rows; the bound for those is |y - y_ref| <= 1e-6 * sum|terms|.
+ * bit-identical to the reference CPU kernel.  SM_ALGO_XBAND keeps that order for
+ * every row as well.  SM_ALGO_AUTO/STREAM and the SpMM kernels keep it for
+ * rows of up to SM_SERIAL_ROW_MAX terms and use a tree sum for longer rows;
+ * the bound for those is |y - y_ref| <= 1e-6 * sum|terms|.
  *
  * Errors: every call returns sm_status; sm_last_error() gives a message for
  * the calling thread.  Device calls are asynchronous on `stream` (a
@@ -64,7 +65,9 @@ typedef enum sm_algo {
     SM_ALGO_AUTO = 0,     /* stream (SpMV) / row-panel (SpMM) kernels              */
     SM_ALGO_PARITY = 1,   /* bit-exact with the reference for every row            */
     SM_ALGO_STREAM = 2,   /* nnz-balanced row tiles through LDS (+ long-row split) */
-    SM_ALGO_VECTOR = 3    /* one wavefront per row, DPP/shuffle reduction          */
+    SM_ALGO_VECTOR = 3,   /* L lanes per row (CSR-vector), shuffle reduction       */
+    SM_ALGO_XBAND = 4     /* x staged through LDS in column bands (bit-exact); falls
+                             back to STREAM when the matrix holds no band layout    */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the
@@ -86,6 +89,8 @@ typedef struct sm_info {
     int32_t n_tiles;            /* stream-kernel row tiles                     */
     int32_t n_long_rows;        /* rows split across workgroups                */
     int32_t max_row_nnz;        /* longest row                                 */
+    int32_t has_xband;          /* 1 if the column-band layout was built       */
+    int32_t xband_blocks, xband_bands;
     int64_t device_bytes;       /* device memory held by the matrix            */
 } sm_info;
 

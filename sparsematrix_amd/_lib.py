@@ -30,7 +30,7 @@ SM_ERR_NO_DEVICE = 7
 
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
-ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3}
+ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
@@ -48,7 +48,8 @@ class SmInfo(C.Structure):
         ("n_cols", C.c_int64), ("nnz", C.c_int64), ("table_size", C.c_int32),
         ("has_ref_stream", C.c_int32), ("n_entries", C.c_int64), ("n_panels", C.c_int64),
         ("device", C.c_int32), ("n_tiles", C.c_int32), ("n_long_rows", C.c_int32),
-        ("max_row_nnz", C.c_int32), ("device_bytes", C.c_int64),
+        ("max_row_nnz", C.c_int32), ("has_xband", C.c_int32), ("xband_blocks", C.c_int32),
+        ("xband_bands", C.c_int32), ("device_bytes", C.c_int64),
     ]
 
 

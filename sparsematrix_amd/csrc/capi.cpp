@@ -14,6 +14,7 @@
 
 #include "encode.h"
 #include "sm_internal.h"
+#include "xband.h"
 
 using namespace smamd;
 
@@ -75,6 +76,10 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.d_long_rows);
     (void)hipFree(m->plan.d_long_ptr);
     (void)hipFree(m->plan.d_chunks);
+    (void)hipFree(m->plan.d_partials);
+    (void)hipFree(m->plan.xb.d_chunk_start);
+    (void)hipFree(m->plan.xb.d_word);
+    (void)hipFree(m->plan.xb.d_val);
     m->d_row_ptr = m->d_col = nullptr;
     m->d_val = nullptr;
     m->plan = Plan();
@@ -83,11 +88,65 @@ void free_device(sm_matrix *m) {
 // Build the stream plan from a host row_ptr and upload it.
 // Tile size: kTileNnz unless SM_TILE_NNZ (1024/2048/4096/8192) overrides it
 // (tuning knob, read at matrix creation).
+// SM_DEBUG_SYNC=1: synchronise after every launch and report the failing call
+// (fault attribution during development; never set in benchmarks).
+bool debug_sync() {
+    static const bool on = [] {
+        const char *e = getenv("SM_DEBUG_SYNC");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
+hipError_t after_launch(hipError_t e, hipStream_t s, const char *what) {
+    if (e != hipSuccess || !debug_sync()) return e;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) fprintf(stderr, "[sparsematrix_amd] %s failed: %s\n", what, hipGetErrorString(e));
+    return e;
+}
+
 int32_t tile_nnz_setting() {
     const char *e = getenv("SM_TILE_NNZ");
     if (!e) return kTileNnz;
     const int v = atoi(e);
     return (v == 1024 || v == 2048 || v == 4096 || v == 8192) ? v : kTileNnz;
+}
+
+// Column-band layout: built when SM_XBAND=1, or by default when x is small
+// enough that sweeping it through every workgroup's LDS costs less than the
+// random gathers it replaces (DESIGN.md "xband").
+bool want_xband(const sm_matrix *m) {
+    const char *e = getenv("SM_XBAND");
+    if (e && atoi(e) == 0) return false;
+    if (m->nnz == 0 || m->n_rows == 0) return false;
+    const int64_t nblk = (m->n_rows + kXbBlockRows - 1) / kXbBlockRows;
+    const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
+    const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
+    if (e && atoi(e) == 1) return true;
+    return x_sweep <= 10.0 * stream && m->n_cols >= kXbBandCols / 2;
+}
+
+sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    XbandHost xh;
+    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, kXbBlockRows, kXbBandCols, xh))
+        return SM_OK;   // layout not applicable: the stream kernel serves this matrix
+    XbandDev &d = m->plan.xb;
+    std::vector<int32_t> cs32(xh.chunk_start.size());
+    for (size_t i = 0; i < cs32.size(); i++) cs32[i] = (int32_t)xh.chunk_start[i];
+    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, (int64_t)cs32.size(), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, (int64_t)xh.word.size(), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_val, (int64_t)xh.val.size(), m->device_bytes));
+    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, cs32.data(), cs32.size() * 4, hipMemcpyHostToDevice));
+    if (!xh.word.empty()) {
+        SM_TRY_HIP(hipMemcpy(d.d_word, xh.word.data(), xh.word.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_val, xh.val.data(), xh.val.size() * 4, hipMemcpyHostToDevice));
+    }
+    d.block_rows = xh.block_rows;
+    d.band_cols = xh.band_cols;
+    d.n_bands = xh.n_bands;
+    d.n_chunks = xh.n_chunks;
+    d.n_blocks = xh.n_blocks;
+    return SM_OK;
 }
 
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
@@ -109,6 +168,7 @@ sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     p.avg_row_nnz = ph.avg_row_nnz;
     SM_TRY_HIP(dev_alloc(&p.d_tiles, p.n_tiles, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_chunks, p.n_chunks, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_partials, p.n_chunks, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_long_rows, p.n_long, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_long_ptr, p.n_long + 1, m->device_bytes));
     if (p.n_tiles)
@@ -158,7 +218,9 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
         SM_TRY_HIP(hipMemcpy(m->d_col, col, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
         SM_TRY_HIP(hipMemcpy(m->d_val, val, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
     }
-    return upload_plan(m, rp);
+    sm_status st2 = upload_plan(m, rp);
+    if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val);
+    return st2;
 }
 
 std::unique_ptr<sm_matrix> new_matrix(int32_t device) {
@@ -355,6 +417,18 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
         return fail(SM_ERR_INVALID_MATRIX, "device CSR failed validation (flags 0x%x)", flag);
     }
     st = upload_plan(m.get(), rp.data());
+    if (st == SM_OK && want_xband(m.get())) {
+        std::vector<int32_t> ch((size_t)nnz);
+        std::vector<float> vh((size_t)nnz);
+        hipError_t e3 = hipSuccess;
+        if (nnz) {
+            e3 = hipMemcpy(ch.data(), m->d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost);
+            if (e3 == hipSuccess)
+                e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
+        }
+        st = e3 == hipSuccess ? upload_xband(m.get(), rp.data(), ch.data(), vh.data())
+                              : hip_fail(e3, "copy CSR for band layout");
+    }
     if (st != SM_OK) { free_device(m.get()); return st; }
     *out = m.release();
     return SM_OK;
@@ -375,6 +449,9 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->n_tiles = m->plan.n_tiles;
     info->n_long_rows = m->plan.n_long;
     info->max_row_nnz = m->plan.max_row_nnz;
+    info->has_xband = m->plan.xb.n_blocks > 0 ? 1 : 0;
+    info->xband_blocks = m->plan.xb.n_blocks;
+    info->xband_bands = m->plan.xb.n_bands;
     info->device_bytes = m->device_bytes;
     return SM_OK;
 }
@@ -475,23 +552,23 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
                                alpha, beta, s);
         break;
     case SM_ALGO_AUTO:
-    case SM_ALGO_STREAM: {
-        float *partials = nullptr;
-        if (m->plan.n_long) {
-            e = hipMallocAsync((void **)&partials, (size_t)m->plan.n_chunks * sizeof(float), s);
-            if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(partials)");
+    case SM_ALGO_XBAND:
+        if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
+            e = launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
+            break;
         }
+        // fall through: no band layout (or unaligned x) -> stream kernel
+        [[fallthrough]];
+    case SM_ALGO_STREAM:
+        // Long-row partial sums live in the matrix (allocated at creation): SpMVs on
+        // one matrix with long rows must not run concurrently on different streams.
         e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
-                               partials, s);
-        if (partials) {
-            hipError_t e2 = hipFreeAsync(partials, s);
-            if (e == hipSuccess) e = e2;
-        }
+                               m->plan.d_partials, s);
         break;
-    }
     default:
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     }
+    e = after_launch(e, s, "sm_spmv");
     return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv launch");
 }
 
@@ -520,6 +597,7 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
                                 alpha, beta, true, s);
     else
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
+    e = after_launch(e, s, "sm_spmm");
     return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmm launch");
 }
 
@@ -542,6 +620,7 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
     // C^T = B A^T, read in place: X(kk, i) = a[i*lda + kk], Y(j, i) = c[i*ldc + j]
     e = launch_spmm_generic((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val, a, 1, lda, c,
                             1, ldc, alpha, beta, false, s);
+    e = after_launch(e, s, "sm_addmatmat");
     return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat launch");
 }
 
@@ -607,12 +686,14 @@ sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t k, cons
     if (!a || !c || !ppos || !pval || !table) return fail(SM_ERR_INVALID_ARG, "null pointer");
     hipStream_t s = (hipStream_t)stream;
     void *ws = nullptr;
-    hipError_t e = hipMallocAsync(&ws, panel_kernel_workspace_bytes(pos_len, n), s);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(panel workspace)");
+    // Not a hot path: a plain allocation, synchronised before it is released.
+    hipError_t e = hipMalloc(&ws, panel_kernel_workspace_bytes(pos_len, n));
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc(panel workspace)");
     e = launch_panel_kernel(variant, m, n, k, a, lda, c, ldc, alpha, ppos, pval, pos_len, table,
                             valid_table_size, ws, s);
-    hipError_t e2 = hipFreeAsync(ws, s);
+    hipError_t e2 = hipStreamSynchronize(s);
     if (e == hipSuccess) e = e2;
+    (void)hipFree(ws);
     return e == hipSuccess ? SM_OK : hip_fail(e, "sm_panel_kernel");
 }
 

@@ -33,7 +33,17 @@ struct alignas(16) Chunk {
     int32_t lr, begin, end, pad;
 };
 
+// Device copy of the column-band layout (xband.h).
+struct XbandDev {
+    int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
+    int64_t n_chunks = 0;
+    int32_t *d_chunk_start = nullptr;
+    uint32_t *d_word = nullptr;
+    float *d_val = nullptr;
+};
+
 struct Plan {
+    XbandDev xb;                      // n_blocks == 0 when not built
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -42,6 +52,7 @@ struct Plan {
     int32_t *d_long_ptr = nullptr;    // n_long + 1 offsets into chunks
     int32_t n_chunks = 0;
     Chunk *d_chunks = nullptr;
+    float *d_partials = nullptr;      // n_chunks long-row partial sums (one SpMV in flight)
     int32_t max_row_nnz = 0;
     double avg_row_nnz = 0.0;
 };
@@ -52,6 +63,8 @@ hipError_t launch_spmv_parity(int32_t n, const int32_t *rp, const int32_t *col, 
 hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *col,
                               const float *val, const float *x, float *y, float alpha,
                               float beta, float *partials, hipStream_t s);
+hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                             float *y, float alpha, float beta, hipStream_t s);
 hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
                               const float *val, const float *x, float *y, float alpha, float beta,
                               hipStream_t s);

@@ -1,0 +1,130 @@
+// xband.cpp -- host-side builder of the column-band layout used by the
+// spmv_xband kernel (kernels_xband.hip).
+//
+// Why: for matrices whose x does not fit the L1, every term of a CSR SpMV is a
+// random 4-byte gather, and on gfx950 those run at <= ~375 G gathers/s chip
+// wide (TA-bound: 64 distinct cache lines per wave instruction) -- far below
+// what HBM delivers for the matrix stream (profiles/r01_microbench.txt).  The
+// band layout replaces the gathers by wide, coalesced loads of x into LDS.
+//
+// Layout.  Rows are cut into blocks of `block_rows` (<= 4096: the per-row
+// accumulators live in LDS); columns into bands of `band_cols` (the x slice
+// staged in LDS).  For block b and band p the block's terms with a column in
+// band p are listed in (row, column) order and packed into chunks of 64
+// entries (one per lane).  A row's run of terms inside one band (its
+// "segment", <= 63 terms) never straddles two chunks: the builder pads the
+// chunk tail with dummy entries instead.  Each entry carries its rank inside
+// its segment, so the kernel can add a chunk's terms to the LDS accumulators in
+// rank rounds -- no two lanes touch one row in the same round, and a row's
+// terms are added in ascending column order across bands and ranks: exactly
+// the reference's order (bit-identical results, no atomics).
+//
+// Entry word: bits [0,14) column in band, [14,20) rank (63 = dummy), [20,32)
+// row in block.  Values are stored beside it (fp32).  chunk_start[b*nb + p]
+// indexes the first chunk of (b, p); chunk_start[nblk*nb] = total chunks.
+#include <algorithm>
+#include <thread>
+
+#include "xband.h"
+
+namespace smamd {
+
+bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
+                 int64_t n_cols, int32_t block_rows, int32_t band_cols, XbandHost &out) {
+    out = XbandHost();
+    if (n_rows <= 0 || n_cols <= 0) return false;
+    if (block_rows > (1 << kXbRowBits) || band_cols > (1 << kXbColBits)) return false;
+    const int64_t nblk = (n_rows + block_rows - 1) / block_rows;
+    const int64_t nb = (n_cols + band_cols - 1) / band_cols;
+    if (nblk * nb >= (int64_t)1 << 31) return false;
+    out.block_rows = block_rows;
+    out.band_cols = band_cols;
+    out.n_blocks = (int32_t)nblk;
+    out.n_bands = (int32_t)nb;
+
+    // Per block: chunks per band (first pass) -> offsets -> fill (second pass).
+    std::vector<int64_t> chunks_of((size_t)(nblk * nb), 0);
+    std::vector<uint8_t> bad((size_t)nblk, 0);
+    const int nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+
+    auto for_blocks = [&](auto &&fn) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthr; t++)
+            th.emplace_back([&, t] {
+                for (int64_t b = t; b < nblk; b += nthr) fn(b);
+            });
+        for (auto &x : th) x.join();
+    };
+
+    // Walk the block's terms band by band.  A cursor per row remembers where
+    // the row's next band starts (columns ascend within a row).
+    auto walk = [&](int64_t b, auto &&emit_seg) {
+        const int64_t r0 = b * block_rows, r1 = std::min<int64_t>(n_rows, r0 + block_rows);
+        std::vector<int32_t> cur((size_t)(r1 - r0));
+        for (int64_t r = r0; r < r1; r++) cur[r - r0] = rp[r];
+        for (int64_t p = 0; p < nb; p++) {
+            const int64_t cend = (p + 1) * band_cols;
+            for (int64_t r = r0; r < r1; r++) {
+                int32_t &c = cur[r - r0];
+                const int32_t s = c;
+                while (c < rp[r + 1] && col[c] < cend) c++;
+                if (c > s) emit_seg(p, (int32_t)(r - r0), s, c);
+            }
+        }
+        for (int64_t r = r0; r < r1; r++)   // unsorted columns would leave terms behind
+            if (cur[r - r0] != rp[r + 1]) return false;
+        return true;
+    };
+
+    for_blocks([&](int64_t b) {
+        std::vector<int32_t> fill((size_t)nb, 0);   // entries used in the open chunk
+        int64_t *cnt = &chunks_of[(size_t)(b * nb)];
+        const bool ok = walk(b, [&](int64_t p, int32_t, int32_t s, int32_t e) {
+            const int32_t len = e - s;
+            if (len > kXbMaxSeg) { bad[b] = 1; return; }
+            if (fill[p] == 0 || fill[p] + len > 64) { cnt[p]++; fill[p] = 0; }
+            fill[p] += len;
+        });
+        if (!ok) bad[b] = 1;
+    });
+    for (int64_t b = 0; b < nblk; b++)
+        if (bad[b]) return false;
+
+    out.chunk_start.resize((size_t)(nblk * nb) + 1);
+    int64_t total = 0;
+    for (size_t i = 0; i < chunks_of.size(); i++) {
+        out.chunk_start[i] = total;
+        total += chunks_of[i];
+    }
+    out.chunk_start.back() = total;
+    if (total * 64 >= (int64_t)1 << 31) return false;
+    out.n_chunks = total;
+    out.word.assign((size_t)(total * 64), kXbDummyWord);
+    out.val.assign((size_t)(total * 64), 0.0f);
+    out.max_chunks_per_band = 0;
+    for (int64_t i = 0; i < nblk * nb; i++)
+        out.max_chunks_per_band = std::max<int64_t>(out.max_chunks_per_band, chunks_of[i]);
+
+    for_blocks([&](int64_t b) {
+        std::vector<int64_t> chunk((size_t)nb), fill((size_t)nb, 0);
+        for (int64_t p = 0; p < nb; p++) chunk[p] = out.chunk_start[(size_t)(b * nb + p)] - 1;
+        walk(b, [&](int64_t p, int32_t rl, int32_t s, int32_t e) {
+            const int32_t len = e - s;
+            if (chunk[p] < out.chunk_start[(size_t)(b * nb + p)] || fill[p] + len > 64) {
+                chunk[p]++;
+                fill[p] = 0;
+            }
+            for (int32_t k = 0; k < len; k++) {
+                const int64_t slot = chunk[p] * 64 + fill[p] + k;
+                const uint32_t cb = (uint32_t)(col[s + k] - p * band_cols);
+                out.word[(size_t)slot] = cb | ((uint32_t)k << kXbColBits) |
+                                         ((uint32_t)rl << (kXbColBits + kXbRankBits));
+                out.val[(size_t)slot] = val[s + k];
+            }
+            fill[p] += len;
+        });
+    });
+    return true;
+}
+
+}  // namespace smamd

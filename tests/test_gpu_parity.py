@@ -379,3 +379,66 @@ def test_panel_kernels_vs_golden(sm):
                                tab.data_ptr(), int(k["table_size"]), None)
         assert st == 0, L.sm_last_error()
         assert bits_equal(to_host(c), k[f"out_v{v}"]), v
+
+
+# ---------------------------------------------------------------------------- column-band kernel
+def _with_env(key, value, fn):
+    import os
+    old = os.environ.get(key)
+    os.environ[key] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = old
+
+
+@pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 300001, 16), (9000, 70001, 40),
+                                                   (4096, 32768, 7), (5000, 1000, 5)])
+def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
+    """LDS-staged column-band SpMV: every row in reference order (bit-exact), incl.
+    partial last band/block, n_cols not a multiple of 4, dense bands (rank rounds)."""
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols)
+    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    info = M.info()
+    assert info["has_xband"] == 1, info
+    rng = np.random.default_rng(1)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (0.5, 0.0)):
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, alpha, beta, algo="xband")
+        assert np.array_equal(bits(to_host(y)), bits(want)), (alpha, beta)
+
+
+def test_xband_not_applicable_falls_back(sm):
+    """A row with > 7 terms inside one band cannot use the layout: the matrix is
+    still served (stream kernel) and results stay correct; unaligned x too."""
+    torch = torch_dev()
+    n_rows, n_cols = 3000, 40000
+    lengths = np.full(n_rows, 3)
+    lengths[17] = 200            # 200 sorted columns in [0, 40000): > 7 per band
+    rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=2)
+    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    assert M.info()["has_xband"] == 0
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 1.0)
+    _, ab = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, x, y0, 1.0, 1.0)
+    y = to_dev(y0)
+    M.spmv(to_dev(x), y, algo="xband")
+    assert_terms_close(to_host(y), want, ab)
+    # unaligned x on a matrix that has the layout
+    rp2, ci2, va2 = uniform_csr(5000, 40000, 8, seed=5)
+    M2 = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp2, ci2, va2, 40000))
+    assert M2.info()["has_xband"] == 1
+    xb = torch.zeros(40001, dtype=torch.float32, device="cuda")
+    xb[1:] = to_dev(x)
+    y = to_dev(y0[:5000].copy())
+    M2.spmv(xb[1:], y, algo="xband")
+    want2 = oracle.csr_spmv(rp2, ci2, va2, x, y0[:5000], 1.0, 1.0)
+    assert np.array_equal(bits(to_host(y)), bits(want2))

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", default="1024,2048,4096,8192")
-    ap.add_argument("--algos", default="vector,parity")
+    ap.add_argument("--algos", default="xband,vector,parity")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
 
@@ -69,8 +69,17 @@ def main():
         mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
         variants.append((f"stream/tile{tsz}", "stream", mats))
     os.environ.pop("SM_TILE_NNZ", None)
+    if "xband" in args.algos.split(","):
+        os.environ["SM_XBAND"] = "1"
+        xmats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
+        os.environ.pop("SM_XBAND")
+        print("xband layout:", {k: xmats[0].info()[k] for k in ("has_xband", "xband_blocks",
+                                                                  "xband_bands")})
+        variants.append(("xband", "xband", xmats))
+    os.environ["SM_XBAND"] = "0"
     base_mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
-    for a in [a for a in args.algos.split(",") if a]:
+    os.environ.pop("SM_XBAND")
+    for a in [a for a in args.algos.split(",") if a and a != "xband"]:
         variants.append((a, a, base_mats))
     info = base_mats[0].info()
 
