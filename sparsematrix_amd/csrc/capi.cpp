@@ -119,6 +119,8 @@ bool want_xband(const sm_matrix *m) {
     const char *e = getenv("SM_XBAND");
     if (e && atoi(e) == 0) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
+    // (the builder may shrink the block height for dense bands; the estimate
+    // uses the largest block)
     const int64_t nblk = (m->n_rows + kXbBlockRows - 1) / kXbBlockRows;
     const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
     const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
@@ -145,6 +147,7 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     d.band_cols = xh.band_cols;
     d.n_bands = xh.n_bands;
     d.n_chunks = xh.n_chunks;
+    d.max_chunks_per_band = xh.max_chunks_per_band;
     d.n_blocks = xh.n_blocks;
     return SM_OK;
 }

@@ -37,6 +37,7 @@ struct alignas(16) Chunk {
 struct XbandDev {
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int64_t n_chunks = 0;
+    int64_t max_chunks_per_band = 0;
     int32_t *d_chunk_start = nullptr;
     uint32_t *d_word = nullptr;
     float *d_val = nullptr;

@@ -29,14 +29,31 @@
 
 namespace smamd {
 
+static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
+                              int64_t n_rows, int64_t n_cols, int32_t block_rows,
+                              int32_t band_cols, XbandHost &out);
+
+// Largest block height (<= block_rows, >= 64) whose bands fit the kernel's
+// register capacity (kXbMaxCap chunks per wave per band).
 bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t block_rows, int32_t band_cols, XbandHost &out) {
+    for (int32_t br = block_rows; br >= 64; br /= 2) {
+        out.too_dense = false;
+        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, band_cols, out)) return true;
+        if (!out.too_dense) return false;   // not a capacity problem: halving will not help
+    }
+    return false;
+}
+
+static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
+                              int64_t n_rows, int64_t n_cols, int32_t block_rows,
+                              int32_t band_cols, XbandHost &out) {
     out = XbandHost();
     if (n_rows <= 0 || n_cols <= 0) return false;
     if (block_rows > (1 << kXbRowBits) || band_cols > (1 << kXbColBits)) return false;
     const int64_t nblk = (n_rows + block_rows - 1) / block_rows;
     const int64_t nb = (n_cols + band_cols - 1) / band_cols;
-    if (nblk * nb >= (int64_t)1 << 31) return false;
+    if (nblk * nb >= (int64_t)1 << 31 || nb > kXbMaxBands) return false;
     out.block_rows = block_rows;
     out.band_cols = band_cols;
     out.n_blocks = (int32_t)nblk;
@@ -99,11 +116,16 @@ bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out.chunk_start.back() = total;
     if (total * 64 >= (int64_t)1 << 31) return false;
     out.n_chunks = total;
-    out.word.assign((size_t)(total * 64), kXbDummyWord);
-    out.val.assign((size_t)(total * 64), 0.0f);
     out.max_chunks_per_band = 0;
     for (int64_t i = 0; i < nblk * nb; i++)
         out.max_chunks_per_band = std::max<int64_t>(out.max_chunks_per_band, chunks_of[i]);
+    // The kernel holds a band's chunks in registers: at most kXbMaxCap per wave.
+    if (out.max_chunks_per_band > (int64_t)kXbMaxCap * (kXbThreads / 64)) {
+        out.too_dense = true;
+        return false;
+    }
+    out.word.assign((size_t)(total * 64), kXbDummyWord);
+    out.val.assign((size_t)(total * 64), 0.0f);
 
     for_blocks([&](int64_t b) {
         std::vector<int64_t> chunk((size_t)nb), fill((size_t)nb, 0);

@@ -44,6 +44,24 @@ def _stream_of(t, stream) -> int:
     return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def _check_dev(t, min_elems: int, name: str) -> None:
+    """Device operand guard: the C ABI takes raw pointers and cannot see sizes."""
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32")
+    if t.numel() < min_elems:
+        raise ValueError(f"{name} has {t.numel()} elements, needs at least {min_elems}")
+
+
+def _check_dev_2d(t, rows: int, cols: int, name: str) -> None:
+    _check_dev(t, 0, name)
+    if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1) or t.shape[0] < rows \
+            or t.shape[1] < cols:
+        raise ValueError(f"{name} must be a row-major {rows} x {cols} (or larger) view")
+
+
 def _algo(algo) -> int:
     if isinstance(algo, int):
         return algo
@@ -211,19 +229,34 @@ class SparseMatrix:
         numpy operands: synchronous and bit-identical to the reference.
         torch cuda operands: asynchronous on the current stream with `algo`."""
         h = self._require()
+        k, n = self.NumRows(), self.NumCols()
+        need_a = (m - 1) * lda + k if (m > 0 and alpha != 0.0 and k > 0) else 0
+        need_c = (m - 1) * ldc + n if (m > 0 and n > 0) else 0
         if _is_device(c):
+            _check_dev(c, need_c, "c")
+            if need_a:
+                _check_dev(a, need_a, "a")
             st = self._L.sm_addmatmat(h, _ptr(a), m, lda, _ptr(c), ldc, alpha, beta, _algo(algo),
                                       _stream_of(c, stream))
         else:
             if not (isinstance(c, np.ndarray) and c.dtype == np.float32 and c.flags.c_contiguous):
                 raise TypeError("host AddMatMat needs C-contiguous float32 numpy arrays")
             a_arr = np.ascontiguousarray(a, np.float32)
+            if c.size < need_c or a_arr.size < need_a:
+                raise ValueError("a or c smaller than the (m, lda/ldc) layout requires")
             st = self._L.sm_addmatmat_host(h, _ptr(a_arr), m, lda, _ptr(c), ldc, alpha, beta)
         check(st, "AddMatMat")
         return c
 
     def spmv(self, x, y, alpha: float = 1.0, beta: float = 1.0, algo="auto", stream=None):
         """y = alpha * B * x + beta * y on device tensors (float32, contiguous)."""
+        inf = self.info()
+        _check_dev(x, inf["n_cols"], "x")
+        _check_dev(y, inf["n_rows"], "y")
+        if (x.dim() != 1 and not x.is_contiguous()) or (y.dim() != 1 and not y.is_contiguous()):
+            raise ValueError("x and y must be contiguous")
+        if x.dim() == 1 and x.stride(0) != 1 or y.dim() == 1 and y.stride(0) != 1:
+            raise ValueError("x and y must be unit-stride")
         st = self._L.sm_spmv(self._require(), alpha, _ptr(x), beta, _ptr(y), _algo(algo),
                              _stream_of(y, stream))
         check(st, "sm_spmv")
@@ -232,6 +265,9 @@ class SparseMatrix:
     def spmm(self, X, Y, alpha: float = 1.0, beta: float = 1.0, algo="auto", stream=None):
         """Y (n x N) = alpha * B * X (k x N) + beta * Y, row-major device tensors."""
         n_rhs = int(Y.shape[1])
+        inf = self.info()
+        _check_dev_2d(X, inf["n_cols"], n_rhs, "X")
+        _check_dev_2d(Y, inf["n_rows"], n_rhs, "Y")
         st = self._L.sm_spmm(self._require(), n_rhs, alpha, _ptr(X), int(X.stride(0)), beta,
                              _ptr(Y), int(Y.stride(0)), _algo(algo), _stream_of(Y, stream))
         check(st, "sm_spmm")

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--tiles", default="1024,2048,4096,8192")
     ap.add_argument("--algos", default="xband,vector,parity")
     ap.add_argument("--json", default="")
+    ap.add_argument("--ablate", default="", help="xband ablation modes (dev), e.g. 1,2,4")
+    ap.add_argument("--opt", default="", help="xband tuning variants (dev), e.g. 0,1,2,3")
     args = ap.parse_args()
 
     import torch
@@ -76,6 +78,10 @@ def main():
         print("xband layout:", {k: xmats[0].info()[k] for k in ("has_xband", "xband_blocks",
                                                                   "xband_bands")})
         variants.append(("xband", "xband", xmats))
+    for a in [int(v) for v in args.ablate.split(",") if v]:
+        variants.append((f"xband/ablate{a}", ("xband", a, None), xmats))
+    for o in [int(v) for v in args.opt.split(",") if v]:
+        variants.append((f"xband/opt{o}", ("xband", 0, o), xmats))
     os.environ["SM_XBAND"] = "0"
     base_mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
     os.environ.pop("SM_XBAND")
@@ -88,6 +94,14 @@ def main():
           for _ in range(args.reps)]
     for rnd in range(args.rounds):
         for name, algo, mats in variants:
+            os.environ.pop("SM_XBAND_ABLATE", None)
+            os.environ.pop("SM_XBAND_OPT", None)
+            if isinstance(algo, tuple):
+                algo, abl, opt = algo
+                if abl:
+                    os.environ["SM_XBAND_ABLATE"] = str(abl)
+                if opt is not None:
+                    os.environ["SM_XBAND_OPT"] = str(opt)
             for i in range(3):
                 d = data[i % len(data)]
                 mats[i % len(mats)].spmv(d[4], d[5], 1.0, 0.5, algo=algo)
