@@ -23,9 +23,12 @@
  * Summation order: SM_ALGO_PARITY adds the terms of every output in stored
  * (ascending column) order, exactly as the reference does, so results are
  * bit-identical to the reference CPU kernel.  SM_ALGO_XBAND keeps that order for
- * every row as well.  SM_ALGO_AUTO/STREAM and the SpMM kernels keep it for
- * rows of up to SM_SERIAL_ROW_MAX terms and use a tree sum for longer rows;
- * the bound for those is |y - y_ref| <= 1e-6 * sum|terms|.
+ * every row on the exact band layout (sm_info.has_xband == 1, or any layout with
+ * xband_slabs == 1); the blocked layout (has_xband == 2) sums each column slab in
+ * order and adds the slab sums in slab order.  SM_ALGO_STREAM and the SpMM
+ * kernels keep the order for rows of up to SM_SERIAL_ROW_MAX terms and use a
+ * tree sum for longer rows.  The bound for every non-exact case is
+ * |y - y_ref| <= 1e-6 * sum|terms|.
  *
  * Errors: every call returns sm_status; sm_last_error() gives a message for
  * the calling thread.  Device calls are asynchronous on `stream` (a
@@ -62,11 +65,12 @@ typedef enum sm_status {
 typedef enum sm_trans { SM_NO_TRANS = 0, SM_TRANS = 1 } sm_trans;
 
 typedef enum sm_algo {
-    SM_ALGO_AUTO = 0,     /* stream (SpMV) / row-panel (SpMM) kernels              */
+    SM_ALGO_AUTO = 0,     /* band layout if built, else stream (SpMV); row-panel (SpMM) */
     SM_ALGO_PARITY = 1,   /* bit-exact with the reference for every row            */
     SM_ALGO_STREAM = 2,   /* nnz-balanced row tiles through LDS (+ long-row split) */
     SM_ALGO_VECTOR = 3,   /* L lanes per row (CSR-vector), shuffle reduction       */
-    SM_ALGO_XBAND = 4     /* x staged through LDS in column bands (bit-exact); falls
+    SM_ALGO_XBAND = 4     /* x staged through LDS in column bands (the layout built at
+                             creation: exact or blocked, see sm_info.has_xband); falls
                              back to STREAM when the matrix holds no band layout    */
 } sm_algo;
 
@@ -89,8 +93,11 @@ typedef struct sm_info {
     int32_t n_tiles;            /* stream-kernel row tiles                     */
     int32_t n_long_rows;        /* rows split across workgroups                */
     int32_t max_row_nnz;        /* longest row                                 */
-    int32_t has_xband;          /* 1 if the column-band layout was built       */
+    int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
+                                   2 blocked (column slabs, Σ|terms| tolerance)  */
     int32_t xband_blocks, xband_bands;
+    int32_t xband_slabs;        /* column slabs per row block (1: bit-identical) */
+    int32_t xband_block_rows;   /* rows per block                              */
     int64_t device_bytes;       /* device memory held by the matrix            */
 } sm_info;
 

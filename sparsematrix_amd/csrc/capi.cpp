@@ -80,6 +80,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.xb.d_chunk_start);
     (void)hipFree(m->plan.xb.d_word);
     (void)hipFree(m->plan.xb.d_val);
+    (void)hipFree(m->plan.xb.d_partials);
     m->d_row_ptr = m->d_col = nullptr;
     m->d_val = nullptr;
     m->plan = Plan();
@@ -112,40 +113,61 @@ int32_t tile_nnz_setting() {
     return (v == 1024 || v == 2048 || v == 4096 || v == 8192) ? v : kTileNnz;
 }
 
-// Column-band layout: built when SM_XBAND=1, or by default when x is small
-// enough that sweeping it through every workgroup's LDS costs less than the
-// random gathers it replaces (DESIGN.md "xband").
+// Column-band layout.  Which one: SM_XBAND=0 disables it,
+// SM_XBAND=1 forces it; otherwise the blocked layout is built when sweeping x
+// through every tile's LDS costs less than the random gathers it replaces.
+// SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
+XbKind xband_kind_setting() {
+    const char *e = getenv("SM_XBAND_KIND");
+    return (e && strcmp(e, "exact") == 0) ? kXbExact : kXbBlocked;
+}
+
 bool want_xband(const sm_matrix *m) {
     const char *e = getenv("SM_XBAND");
     if (e && atoi(e) == 0) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
-    // (the builder may shrink the block height for dense bands; the estimate
-    // uses the largest block)
-    const int64_t nblk = (m->n_rows + kXbBlockRows - 1) / kXbBlockRows;
+    if (e && atoi(e) == 1) return true;
+    const int rows_log2 = xband_kind_setting() == kXbExact ? kXbExactRowsLog2 : kXbBlockedRowsLog2;
+    const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
     const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
     const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
-    if (e && atoi(e) == 1) return true;
-    return x_sweep <= 10.0 * stream && m->n_cols >= kXbBandCols / 2;
+    return x_sweep <= 10.0 * stream && m->n_cols >= 8192;
 }
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    const XbKind kind = xband_kind_setting();
+    const XbBits bits = kind == kXbExact ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
+                                         : xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
     XbandHost xh;
-    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, kXbBlockRows, kXbBandCols, xh))
+    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, xh))
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     XbandDev &d = m->plan.xb;
+    // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
+    int32_t n_slabs = 1;
+    if (kind == kXbBlocked) {
+        const int64_t want = (kXbTargetTiles + xh.n_blocks - 1) / xh.n_blocks;
+        n_slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(want, xh.n_bands));
+    }
+    const int32_t slab_bands = (xh.n_bands + n_slabs - 1) / n_slabs;
+    n_slabs = (xh.n_bands + slab_bands - 1) / slab_bands;
     std::vector<int32_t> cs32(xh.chunk_start.size());
     for (size_t i = 0; i < cs32.size(); i++) cs32[i] = (int32_t)xh.chunk_start[i];
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, (int64_t)cs32.size(), m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_word, (int64_t)xh.word.size(), m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_val, (int64_t)xh.val.size(), m->device_bytes));
+    if (n_slabs > 1)
+        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(n_slabs - 1) * m->n_rows, m->device_bytes));
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, cs32.data(), cs32.size() * 4, hipMemcpyHostToDevice));
     if (!xh.word.empty()) {
         SM_TRY_HIP(hipMemcpy(d.d_word, xh.word.data(), xh.word.size() * 4, hipMemcpyHostToDevice));
         SM_TRY_HIP(hipMemcpy(d.d_val, xh.val.data(), xh.val.size() * 4, hipMemcpyHostToDevice));
     }
+    d.kind = kind;
     d.block_rows = xh.block_rows;
     d.band_cols = xh.band_cols;
     d.n_bands = xh.n_bands;
+    d.n_slabs = n_slabs;
+    d.slab_bands = slab_bands;
     d.n_chunks = xh.n_chunks;
     d.max_chunks_per_band = xh.max_chunks_per_band;
     d.n_blocks = xh.n_blocks;
@@ -452,9 +474,11 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->n_tiles = m->plan.n_tiles;
     info->n_long_rows = m->plan.n_long;
     info->max_row_nnz = m->plan.max_row_nnz;
-    info->has_xband = m->plan.xb.n_blocks > 0 ? 1 : 0;
+    info->has_xband = m->plan.xb.n_blocks > 0 ? m->plan.xb.kind : 0;
     info->xband_blocks = m->plan.xb.n_blocks;
     info->xband_bands = m->plan.xb.n_bands;
+    info->xband_slabs = m->plan.xb.n_blocks > 0 ? m->plan.xb.n_slabs : 0;
+    info->xband_block_rows = m->plan.xb.block_rows;
     info->device_bytes = m->device_bytes;
     return SM_OK;
 }

@@ -1,17 +1,26 @@
 // kernels_xband.hip -- SpMV with x staged through LDS, one column band at a time.
 //
-// One workgroup (1024 threads, 16 waves) per block of <= 4096 rows, one
-// workgroup per CU.  LDS: two x bands (2 x 16384 floats = 128 KiB) and the
-// block's accumulators (4096 floats = 16 KiB).  Software pipeline, one barrier
-// per band: while band p is applied from one buffer, slice p+1 (held in
-// registers since two bands earlier, wide float4 loads) is written to the other
-// while slice p+3 and the entries of band p+3 are in flight.  Each wave takes whole 64-entry
+// One workgroup (1024 threads, 16 waves) per tile = (block of rows, slab of
+// column bands), one workgroup per CU.  LDS: two x bands (double-buffered) and
+// the block's accumulators.  Software pipeline, one barrier per band: while
+// band p is applied from one buffer, slice p+1 (held in registers since two
+// bands earlier, wide float4 loads) is written to the other while slice p+3
+// and the entries of band p+3 are in flight.  Each wave takes whole 64-entry
 // chunks: term = x_lds[col] * (v * alpha), then the chunk's terms are added to
 // the LDS accumulators in rank rounds (no two lanes touch one row in a round;
-// no atomics).
-// A row's terms are therefore added in ascending column order (bands ascend,
-// ranks ascend inside a band), starting from beta*y: bit-identical to the
-// reference.  Layout and its builder: xband.h / xband.cpp.
+// no atomics).  Inside a tile a row's terms are therefore added in ascending
+// column order (bands ascend, ranks ascend inside a band).
+//
+// Slab 0 starts from beta*y and writes y; slab s > 0 starts from 0 and writes
+// partials[s-1]; combine_slabs_kernel then adds the partials to y in slab
+// order.  With one slab (the "exact" layout) every row is summed exactly in the
+// reference's order: bit-identical.  Layout and builder: xband.h / xband.cpp.
+//
+// Why x goes through LDS (profiles/r01_microbench.txt): random 4-byte gathers
+// are TA-bound (~0.6 lanes/clk/CU); wide loads of a band are not.  The cost is
+// that every tile sweeps its slab of x: blocked tiles (16K rows) sweep 4x less
+// x per CU than exact ones (4K rows) -- the x sweep, L2 -> CU at ~85 GB/s per
+// CU, is what bounds the exact layout.
 #include "sm_internal.h"
 #include "xband.h"
 
@@ -32,44 +41,55 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 
-
-
-// ABL (ablation, development only): bit 1 skips the apply, bit 2 the x slice loads,
-// bit 4 the entry loads (values kept live so nothing upstream is dead-code removed).
-// OPT (tuning variants): bit 1 pads the accumulator rows, bit 2 skips all-dummy chunks.
-template <int THREADS, int BAND, int BROWS, int CAP, int MAXB, int ABL = 0, int OPT = 0>
+// ABL (ablation, development only, SM_XBAND_ABLATE): bit 1 skips the apply, bit 2
+// the x slice loads, bit 4 the entry loads, bit 16 the per-band barrier; the staged
+// slices are kept live so nothing upstream is dead-code removed.  Timing only:
+// results are wrong.
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
-    int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands,
-    const int32_t *__restrict__ chunk_start,
+    int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
+    int32_t slab_bands, const int32_t *__restrict__ chunk_start,
     const uint32_t *__restrict__ word, const float *__restrict__ val,
-    const float *__restrict__ x, float *__restrict__ y, float alpha, float beta) {
+    const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
+    float alpha, float beta) {
+    constexpr int BAND = 1 << BAND_LOG2;
+    constexpr int BROWS = 1 << ROWS_LOG2;
+    constexpr XbBits kBits = xb_bits(BAND_LOG2, ROWS_LOG2);
+    constexpr uint32_t kColMask = (1u << kBits.col) - 1u;
+    constexpr uint32_t kRankMask = (1u << kBits.rank) - 1u;
+    constexpr uint32_t kDummyRank = kBits.dummy_rank();
+    constexpr uint32_t kDummyWord = kBits.dummy_word();
     constexpr int kWaves = THREADS / 64;
     constexpr int kXv = BAND / (4 * THREADS);   // float4 per thread per band
     static_assert(kXv >= 1, "band too small for the workgroup");
     __shared__ __attribute__((aligned(16))) float xs[2][BAND];
-    __shared__ float yacc[BROWS + BROWS / 32];   // OPT&1: one pad word per 32 rows
-    auto yslot = [](uint32_t r) -> uint32_t { return (OPT & 1) ? r + (r >> 5) : r; };
+    __shared__ float yacc[BROWS];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int32_t b = blockIdx.x;
+    const int32_t b = blockIdx.x / n_slabs;
+    const int32_t slab = blockIdx.x - b * n_slabs;
+    const int32_t p_first = slab * slab_bands;
+    const int32_t nb = min(slab_bands, n_bands - p_first);   // bands of this tile (>= 1)
     const int32_t r0 = b * block_rows;
     const int32_t nr = min(block_rows, n_rows - r0);
-    const int32_t *csg = chunk_start + (int64_t)b * n_bands;
+    const int32_t *csg = chunk_start + (int64_t)b * n_bands + p_first;
     const int32_t c_first = csg[0];
-    const int32_t c_last = csg[n_bands];
-    const __amdgpu_buffer_rsrc_t xr_src = rsrc(x, (uint64_t)n_cols * 4);
+    const int32_t c_last = csg[nb];
+    const int64_t x0 = (int64_t)p_first * BAND;
+    const __amdgpu_buffer_rsrc_t xr_src = rsrc(x + x0, (uint64_t)(n_cols - x0) * 4);
     const __amdgpu_buffer_rsrc_t w_src =
         rsrc(word + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
     const __amdgpu_buffer_rsrc_t v_src =
         rsrc(val + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
+    float *out = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * n_rows + r0;
     // Chunk table window in registers: lane l holds cs[cw + l] and cs[cw + 64 + l]
-    // (block-relative); scalar reads via readlane, reloaded every 64 bands.
+    // (tile-relative); scalar reads via readlane, reloaded every 124 bands.
     int32_t cw = 0;
     int32_t cs_lo = 0, cs_hi = 0;
     auto load_cs_window = [&](int32_t base) {
         cw = base;
-        const int32_t i0 = min(base + lane, n_bands), i1 = min(base + 64 + lane, n_bands);
+        const int32_t i0 = min(base + lane, nb), i1 = min(base + 64 + lane, nb);
         cs_lo = csg[i0] - c_first;
         cs_hi = csg[i1] - c_first;
     };
@@ -96,19 +116,19 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     };
     // Chunk c of band p for this wave (c beyond the band -> dummy after the load).
     auto load_entries = [&](int32_t p, uint32_t *w, float *v) {
-        const bool inb = p < n_bands;
+        const bool inb = p < nb;
         const int32_t c0 = inb ? cs_at(p) : 0;
         const int32_t c1 = inb ? cs_at(p + 1) : 0;
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
             const int32_t c = c0 + wave + k * kWaves;
             const uint32_t off = 4u * (uint32_t)(c * 64 + lane);
-            uint32_t wl = (uint32_t)(lane * 131) & 0x3fffu, vl = off;
+            uint32_t wl = (uint32_t)(lane * 131) & kColMask, vl = off;
             if (!(ABL & 4)) {
                 wl = __builtin_amdgcn_raw_buffer_load_b32(w_src, off, 0, kAuxNt);
                 vl = __builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, kAuxNt);
             }
-            w[k] = c < c1 ? wl : kXbDummyWord;
+            w[k] = c < c1 ? wl : kDummyWord;
             v[k] = __uint_as_float(vl);
         }
     };
@@ -121,19 +141,12 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         uint32_t rk[CAP], rl[CAP];
         bool live[CAP];
         bool more = false;
-        int kmax = 0;   // chunks of this wave holding live entries (wave-uniform)
-#pragma unroll
-        for (int k = 0; k < CAP; ++k)
-            if (!(OPT & 2) ||
-                __any(((wa[k] >> kXbColBits) & ((1u << kXbRankBits) - 1u)) != kXbDummyRank))
-                kmax = k + 1;
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
-            if (k >= kmax) { live[k] = false; rk[k] = 0; rl[k] = 0; xv[k] = 0.0f; yv[k] = 0.0f; continue; }
-            rk[k] = (wa[k] >> kXbColBits) & ((1u << kXbRankBits) - 1u);
-            live[k] = rk[k] != kXbDummyRank;
-            const uint32_t cl = live[k] ? (wa[k] & ((1u << kXbColBits) - 1u)) : 0u;
-            rl[k] = live[k] ? yslot(wa[k] >> (kXbColBits + kXbRankBits)) : 0u;
+            rk[k] = (wa[k] >> kBits.col) & kRankMask;
+            live[k] = rk[k] != kDummyRank;
+            const uint32_t cl = live[k] ? (wa[k] & kColMask) : 0u;
+            rl[k] = live[k] ? wa[k] >> (kBits.col + kBits.rank) : 0u;
             xv[k] = xb[cl];
             yv[k] = yacc[rl[k]];
             more |= live[k] && rk[k] > 0;
@@ -141,7 +154,6 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         float t[CAP];
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
-            if (k >= kmax) { t[k] = 0.0f; continue; }
             t[k] = __fmul_rn(xv[k], __fmul_rn(va[k], alpha));
             if (live[k] && rk[k] == 0) yacc[rl[k]] = __fadd_rn(yv[k], t[k]);
         }
@@ -167,11 +179,13 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     float V0[CAP], V1[CAP], V2[CAP], V3[CAP];
     load_slice(0, X0);
     for (int32_t i = tid; i < nr; i += THREADS) {
-        float v = y[r0 + i];
-        if (beta != 1.0f) v = __fmul_rn(v, beta);
-        yacc[yslot(i)] = v;
+        float v = 0.0f;
+        if (slab == 0) {
+            v = y[r0 + i];
+            if (beta != 1.0f) v = __fmul_rn(v, beta);
+        }
+        yacc[i] = v;
     }
-    __syncthreads();   // cs[] visible
     load_entries(0, W0, V0);
     load_entries(1, W1, V1);
     load_entries(2, W2, V2);
@@ -184,14 +198,13 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // One barrier per band: the stores of slice p+1 into buffer (p+1)&1 (freed
     // by the previous barrier) and this band's reads of buffer p&1 both finish
     // before it.  Slice p+3 reuses the register set just stored; entries of
-    // band p+3 reuse the set of band p-1.  Loads past the last band read zeros
-    // (range-checked descriptors) and are never applied.
+    // band p+3 reuse the set of band p-1.  Loads past the tile's last band read
+    // the next slab's data or zeros (range-checked descriptors) and are never applied.
     auto step = [&](int32_t p, float4 *xnext, uint32_t *wa, float *va, uint32_t *wl, float *vl) {
-        if (p + 4 >= cw + 128) load_cs_window(p);   // every 124 bands (n_bands > 124 only)
+        if (p + 4 >= cw + 128) load_cs_window(p);   // every 124 bands (nb > 124 only)
         store_slice((p + 1) & 1, xnext);
         load_slice(p + 3, xnext);
         load_entries(p + 3, wl, vl);
-        const float *xbuf = xs[p & 1];
         // Every chunk of the band is in registers: the builder guarantees at
         // most CAP chunks per wave per band (no loop of loads in the pipeline,
         // so hipcc can count vmcnt exactly).
@@ -199,80 +212,90 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 #pragma unroll
             for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
         } else {
-            apply_band(xbuf, wa, va);
+            apply_band(xs[p & 1], wa, va);
         }
-        __syncthreads();
+        if (!(ABL & 16)) __syncthreads();
     };
-    for (int32_t p = 0; p < n_bands; p += 4) {
+    for (int32_t p = 0; p < nb; p += 4) {
         step(p, X1, W0, V0, W3, V3);
-        if (p + 1 >= n_bands) break;
+        if (p + 1 >= nb) break;
         step(p + 1, X0, W1, V1, W0, V0);
-        if (p + 2 >= n_bands) break;
+        if (p + 2 >= nb) break;
         step(p + 2, X1, W2, V2, W1, V1);
-        if (p + 3 >= n_bands) break;
+        if (p + 3 >= nb) break;
         step(p + 3, X0, W3, V3, W2, V2);
     }
-    for (int32_t i = tid; i < nr; i += THREADS) y[r0 + i] = yacc[yslot(i)];
+    for (int32_t i = tid; i < nr; i += THREADS) out[i] = yacc[i];
+    if (ABL && beta == -12345.0f) y[tid] = xs[0][tid] + xs[1][tid];   // keep the staging live
+}
+
+// y[r] = (((y[r] + p_0[r]) + p_1[r]) + ...): the slab partial sums in slab order.
+__global__ __launch_bounds__(256) void combine_slabs_kernel(int32_t n_rows, int32_t n_parts,
+                                                            const float *__restrict__ partials,
+                                                            float *__restrict__ y) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n_rows) return;
+    float acc = y[r];
+    for (int32_t s = 0; s < n_parts; ++s) acc = __fadd_rn(acc, partials[(int64_t)s * n_rows + r]);
+    y[r] = acc;
+}
+
+template <int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
+hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                        float *y, float alpha, float beta, hipStream_t s) {
+    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, ABL>),
+                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s,
+                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,
+                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, alpha, beta);
+    return hipGetLastError();
+}
+
+template <int BAND_LOG2, int ROWS_LOG2>
+hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                       float *y, float alpha, float beta, hipStream_t s) {
+    const int waves = kXbThreads / 64;
+    const int64_t cap = (xb.max_chunks_per_band + waves - 1) / waves;
+    const char *abl_env = getenv("SM_XBAND_ABLATE");   // development only
+    const int abl = abl_env ? atoi(abl_env) : 0;
+    if (abl) {
+        if (cap > 2) return hipErrorInvalidValue;
+        switch (abl) {
+        case 1: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 2: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 4: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 5: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 16: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (cap <= 1) return launch_tiles<BAND_LOG2, ROWS_LOG2, 1, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 2) return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= kXbMaxCap) return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-constexpr int kXbDefaultOpt = 0;
-
-bool cap_fits(const XbandDev &xb, int cap) {
-    return xb.max_chunks_per_band <= (int64_t)cap * (kXbThreads / 64);
-}
-
 hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s) {
     if (xb.n_blocks <= 0) return hipSuccess;
-    if (xb.block_rows > kXbBlockRows || xb.band_cols != kXbBandCols ||
-        xb.n_bands > kXbMaxBands)
+    if (xb.n_bands > kXbMaxBands || xb.n_slabs < 1 || xb.slab_bands < 1 ||
+        (int64_t)xb.n_slabs * xb.slab_bands < xb.n_bands ||
+        (int64_t)(xb.n_slabs - 1) * xb.slab_bands >= xb.n_bands ||
+        (xb.n_slabs > 1 && !xb.d_partials))
         return hipErrorInvalidValue;
-    const int waves = kXbThreads / 64;
-    const int64_t cap = (xb.max_chunks_per_band + waves - 1) / waves;
-    const char *abl_env = getenv("SM_XBAND_ABLATE");
-    const int abl = abl_env ? atoi(abl_env) : 0;
-    const char *opt_env = getenv("SM_XBAND_OPT");
-    const int opt = opt_env ? atoi(opt_env) : kXbDefaultOpt;
-    if (opt != kXbDefaultOpt && abl == 0 && cap_fits(xb, 2)) {   // development variants
-        switch (opt) {
-#define SM_XBO(O)                                                                                 \
-    case O:                                                                                       \
-        hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, kXbBandCols, kXbBlockRows, 2, kXbMaxBands, 0, O>), \
-                           dim3((unsigned)xb.n_blocks), dim3(kXbThreads), 0, s, n_rows, n_cols,     \
-                           xb.block_rows, xb.n_bands, xb.d_chunk_start, xb.d_word, xb.d_val, x, y, \
-                           alpha, beta);                                                          \
-        return hipGetLastError();
-            SM_XBO(0) SM_XBO(1) SM_XBO(2) SM_XBO(3)
-#undef SM_XBO
-        default: return hipErrorInvalidValue;
-        }
-    }
-    if (abl) {   // development-only ablations (never the product path)
-        switch (abl) {
-#define SM_XBA(A)                                                                                 \
-    case A:                                                                                       \
-        hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, kXbBandCols, kXbBlockRows, 2, kXbMaxBands, A>), \
-                           dim3((unsigned)xb.n_blocks), dim3(kXbThreads), 0, s, n_rows, n_cols,     \
-                           xb.block_rows, xb.n_bands, xb.d_chunk_start, xb.d_word, xb.d_val, x, y, \
-                           alpha, beta);                                                          \
-        break;
-            SM_XBA(1) SM_XBA(2) SM_XBA(3) SM_XBA(4) SM_XBA(5) SM_XBA(6) SM_XBA(7)
-#undef SM_XBA
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-#define SM_XB(C)                                                                               \
-    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, kXbBandCols, kXbBlockRows, C, kXbMaxBands>), \
-                       dim3((unsigned)xb.n_blocks), dim3(kXbThreads), 0, s, n_rows, n_cols,     \
-                       xb.block_rows, xb.n_bands, xb.d_chunk_start, xb.d_word, xb.d_val, x, y, alpha, beta)
-    if (cap <= 1) SM_XB(1);
-    else if (cap <= 2) SM_XB(2);
-    else if (cap <= kXbMaxCap) SM_XB(4);
-    else return hipErrorInvalidValue;
-#undef SM_XB
+    hipError_t e;
+    if (xb.kind == kXbExact && xb.band_cols == 1 << kXbExactBandLog2 &&
+        xb.block_rows <= 1 << kXbExactRowsLog2)
+        e = launch_kind<kXbExactBandLog2, kXbExactRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    else if (xb.kind == kXbBlocked && xb.band_cols == 1 << kXbBlockedBandLog2 &&
+             xb.block_rows <= 1 << kXbBlockedRowsLog2)
+        e = launch_kind<kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    else
+        return hipErrorInvalidValue;
+    if (e != hipSuccess || xb.n_slabs == 1) return e;
+    hipLaunchKernelGGL(combine_slabs_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
+                       n_rows, xb.n_slabs - 1, (const float *)xb.d_partials, y);
     return hipGetLastError();
 }
 

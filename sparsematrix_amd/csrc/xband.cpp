@@ -19,9 +19,10 @@
 // terms are added in ascending column order across bands and ranks: exactly
 // the reference's order (bit-identical results, no atomics).
 //
-// Entry word: bits [0,14) column in band, [14,20) rank (63 = dummy), [20,32)
-// row in block.  Values are stored beside it (fp32).  chunk_start[b*nb + p]
-// indexes the first chunk of (b, p); chunk_start[nblk*nb] = total chunks.
+// Entry word: column in band | rank (all ones = dummy) | row in block, with
+// field widths from XbBits (xband.h).  Values are stored beside it (fp32).
+// chunk_start[b*nb + p] indexes the first chunk of (b, p); chunk_start[nblk*nb]
+// = total chunks.
 #include <algorithm>
 #include <thread>
 
@@ -30,27 +31,30 @@
 namespace smamd {
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
-                              int64_t n_rows, int64_t n_cols, int32_t block_rows,
-                              int32_t band_cols, XbandHost &out);
+                              int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
+                              XbandHost &out);
 
-// Largest block height (<= block_rows, >= 64) whose bands fit the kernel's
+// Largest block height (<= 2^bits.row, >= 64) whose bands fit the kernel's
 // register capacity (kXbMaxCap chunks per wave per band).
 bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t block_rows, int32_t band_cols, XbandHost &out) {
-    for (int32_t br = block_rows; br >= 64; br /= 2) {
+                 int64_t n_cols, XbBits bits, XbandHost &out) {
+    if (bits.col < 8 || bits.row < 6 || bits.rank < 2 || bits.col + bits.rank + bits.row != 32)
+        return false;
+    for (int32_t br = 1 << bits.row; br >= 64; br /= 2) {
         out.too_dense = false;
-        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, band_cols, out)) return true;
+        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, bits, out)) return true;
         if (!out.too_dense) return false;   // not a capacity problem: halving will not help
     }
     return false;
 }
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
-                              int64_t n_rows, int64_t n_cols, int32_t block_rows,
-                              int32_t band_cols, XbandHost &out) {
+                              int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
+                              XbandHost &out) {
     out = XbandHost();
     if (n_rows <= 0 || n_cols <= 0) return false;
-    if (block_rows > (1 << kXbRowBits) || band_cols > (1 << kXbColBits)) return false;
+    const int32_t band_cols = 1 << bits.col;
+    out.bits = bits;
     const int64_t nblk = (n_rows + block_rows - 1) / block_rows;
     const int64_t nb = (n_cols + band_cols - 1) / band_cols;
     if (nblk * nb >= (int64_t)1 << 31 || nb > kXbMaxBands) return false;
@@ -98,7 +102,7 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
         int64_t *cnt = &chunks_of[(size_t)(b * nb)];
         const bool ok = walk(b, [&](int64_t p, int32_t, int32_t s, int32_t e) {
             const int32_t len = e - s;
-            if (len > kXbMaxSeg) { bad[b] = 1; return; }
+            if (len >= bits.max_seg()) { bad[b] = 1; return; }
             if (fill[p] == 0 || fill[p] + len > 64) { cnt[p]++; fill[p] = 0; }
             fill[p] += len;
         });
@@ -124,7 +128,7 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
         out.too_dense = true;
         return false;
     }
-    out.word.assign((size_t)(total * 64), kXbDummyWord);
+    out.word.assign((size_t)(total * 64), bits.dummy_word());
     out.val.assign((size_t)(total * 64), 0.0f);
 
     for_blocks([&](int64_t b) {
@@ -139,8 +143,8 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
             for (int32_t k = 0; k < len; k++) {
                 const int64_t slot = chunk[p] * 64 + fill[p] + k;
                 const uint32_t cb = (uint32_t)(col[s + k] - p * band_cols);
-                out.word[(size_t)slot] = cb | ((uint32_t)k << kXbColBits) |
-                                         ((uint32_t)rl << (kXbColBits + kXbRankBits));
+                out.word[(size_t)slot] = cb | ((uint32_t)k << bits.col) |
+                                         ((uint32_t)rl << (bits.col + bits.rank));
                 out.val[(size_t)slot] = val[s + k];
             }
             fill[p] += len;

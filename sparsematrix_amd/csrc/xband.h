@@ -6,19 +6,35 @@
 
 namespace smamd {
 
-constexpr int kXbColBits = 14;                 // column inside a band: band_cols <= 16384
-constexpr int kXbRankBits = 6;                 // rank inside the row's segment
-constexpr int kXbRowBits = 12;                 // row inside a block: block_rows <= 4096
-constexpr int kXbMaxSeg = 63;                  // ranks 0..62; 63 marks a dummy
-constexpr uint32_t kXbDummyRank = 63u;
-constexpr uint32_t kXbDummyWord = kXbDummyRank << kXbColBits;
-constexpr int kXbBandCols = 16384;             // 64 KiB of x per band, double-buffered in LDS
-constexpr int kXbBlockRows = 4096;             // 16 KiB of accumulators in LDS
+// Entry word: bits [0, C) column in band, [C, C+K) rank inside the row's segment
+// (all ones = dummy), [C+K, 32) row in block; C = log2(band_cols), R = log2(max
+// block height), K = 32 - C - R.
+struct XbBits {
+    int col, rank, row;
+    constexpr uint32_t dummy_rank() const { return (1u << rank) - 1u; }
+    constexpr uint32_t dummy_word() const { return dummy_rank() << col; }
+    constexpr int max_seg() const { return (1 << rank) - 1; }   // ranks 0 .. max_seg-1
+};
+constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
+    return XbBits{band_cols_log2, 32 - band_cols_log2 - block_rows_log2, block_rows_log2};
+}
+
+// Two layouts over the same builder and kernel:
+//  exact   -- 4096-row blocks, 16384-column bands, the whole x per block: every row
+//             summed in the reference's order (bit-identical);
+//  blocked -- 16384-row blocks, 8192-column bands, columns split in slabs so each
+//             workgroup stages 4x less x; slab partial sums are combined in slab
+//             order (within the Σ|terms| tolerance, bit-identical with one slab).
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2 };
+constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
+constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbThreads = 1024;               // one workgroup per CU
-constexpr int kXbMaxBands = 2048;              // chunk table in LDS: n_cols <= 32 M
+constexpr int kXbMaxBands = 4096;              // n_cols <= 32 M (blocked) / 64 M (exact)
 constexpr int kXbMaxCap = 4;                   // chunks per wave per band held in registers
+constexpr int kXbTargetTiles = 256;            // blocked: >= one tile per CU
 
 struct XbandHost {
+    XbBits bits{0, 0, 0};
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int64_t n_chunks = 0;
     int64_t max_chunks_per_band = 0;
@@ -29,10 +45,10 @@ struct XbandHost {
 };
 
 // Returns false when the matrix does not fit the layout (a row segment longer
-// than kXbMaxSeg inside one band, unsorted columns, bands too dense even for
-// 64-row blocks, or size limits).  `block_rows` is the largest block height
-// tried; the result's block_rows may be smaller.
+// than bits.max_seg()-1 inside one band, unsorted columns, bands too dense even
+// for 64-row blocks, or size limits).  The block height starts at 2^bits.row and
+// halves while a band overflows the kernel's register capacity.
 bool xband_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t block_rows, int32_t band_cols, XbandHost &out);
+                 int64_t n_cols, XbBits bits, XbandHost &out);
 
 }  // namespace smamd

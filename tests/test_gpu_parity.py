@@ -401,9 +401,10 @@ def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
     """LDS-staged column-band SpMV: every row in reference order (bit-exact), incl.
     partial last band/block, n_cols not a multiple of 4, dense bands (rank rounds)."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols)
-    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    M = _with_env("SM_XBAND_KIND", "exact", lambda: _with_env(
+        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
     info = M.info()
-    assert info["has_xband"] == 1, info
+    assert info["has_xband"] == 1 and info["xband_slabs"] == 1, info
     rng = np.random.default_rng(1)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
@@ -414,13 +415,42 @@ def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
         assert np.array_equal(bits(to_host(y)), bits(want)), (alpha, beta)
 
 
+@pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 300001, 16), (9000, 70001, 40),
+                                                   (70000, 1000003, 16), (5000, 1000, 5),
+                                                   (40000, 20000, 3)])
+def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row):
+    """Blocked band layout (16K-row blocks, column slabs): within the Σ|terms| bound
+    of the reference order; bit-identical when the matrix is a single slab; the
+    AUTO path runs it; beta = 0 drops NaN only where the reference does."""
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols + 7)
+    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    info = M.info()
+    assert info["has_xband"] == 2, info
+    assert info["xband_block_rows"] >= 64 and info["xband_slabs"] >= 1
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    y0[::97] = np.nan
+    for alpha, beta, algo in ((1.0, 1.0, "xband"), (1.3, 0.7, "auto"), (0.5, 0.0, "xband")):
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, alpha, beta, algo=algo)
+        got = to_host(y)
+        if info["xband_slabs"] == 1:
+            assert np.array_equal(bits(got), bits(want)), (alpha, beta)
+        else:
+            assert_terms_close(got, want, absum)
+
+
 def test_xband_not_applicable_falls_back(sm):
-    """A row with > 7 terms inside one band cannot use the layout: the matrix is
-    still served (stream kernel) and results stay correct; unaligned x too."""
+    """A row with more terms inside one band than the rank field holds cannot use the
+    layout: the matrix is still served (stream kernel) and results stay correct;
+    unaligned x too."""
     torch = torch_dev()
     n_rows, n_cols = 3000, 40000
     lengths = np.full(n_rows, 3)
-    lengths[17] = 200            # 200 sorted columns in [0, 40000): > 7 per band
+    lengths[17] = 200            # 200 sorted columns in [0, 40000): ~41 per 8192-column band
     rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=2)
     M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
     assert M.info()["has_xband"] == 0
@@ -435,7 +465,7 @@ def test_xband_not_applicable_falls_back(sm):
     # unaligned x on a matrix that has the layout
     rp2, ci2, va2 = uniform_csr(5000, 40000, 8, seed=5)
     M2 = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp2, ci2, va2, 40000))
-    assert M2.info()["has_xband"] == 1
+    assert M2.info()["has_xband"] == 2
     xb = torch.zeros(40001, dtype=torch.float32, device="cuda")
     xb[1:] = to_dev(x)
     y2 = rng.uniform(-1, 1, 5000).astype(np.float32)

@@ -34,7 +34,6 @@ def main():
     ap.add_argument("--algos", default="xband,vector,parity")
     ap.add_argument("--json", default="")
     ap.add_argument("--ablate", default="", help="xband ablation modes (dev), e.g. 1,2,4")
-    ap.add_argument("--opt", default="", help="xband tuning variants (dev), e.g. 0,1,2,3")
     args = ap.parse_args()
 
     import torch
@@ -71,21 +70,25 @@ def main():
         mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
         variants.append((f"stream/tile{tsz}", "stream", mats))
     os.environ.pop("SM_TILE_NNZ", None)
-    if "xband" in args.algos.split(","):
+    xmats = None
+    for kind, name in (("blocked", "xband"), ("exact", "exact")):
+        if name not in args.algos.split(","):
+            continue
         os.environ["SM_XBAND"] = "1"
-        xmats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
+        os.environ["SM_XBAND_KIND"] = kind
+        mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
         os.environ.pop("SM_XBAND")
-        print("xband layout:", {k: xmats[0].info()[k] for k in ("has_xband", "xband_blocks",
-                                                                  "xband_bands")})
-        variants.append(("xband", "xband", xmats))
+        os.environ.pop("SM_XBAND_KIND")
+        print(f"{name} layout:", {k: mats[0].info()[k] for k in (
+            "has_xband", "xband_blocks", "xband_bands", "xband_slabs", "xband_block_rows")})
+        variants.append((name, "xband", mats))
+        xmats = xmats or mats
     for a in [int(v) for v in args.ablate.split(",") if v]:
-        variants.append((f"xband/ablate{a}", ("xband", a, None), xmats))
-    for o in [int(v) for v in args.opt.split(",") if v]:
-        variants.append((f"xband/opt{o}", ("xband", 0, o), xmats))
+        variants.append((f"xband/ablate{a}", ("xband", a), xmats))
     os.environ["SM_XBAND"] = "0"
     base_mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
     os.environ.pop("SM_XBAND")
-    for a in [a for a in args.algos.split(",") if a and a != "xband"]:
+    for a in [a for a in args.algos.split(",") if a and a not in ("xband", "exact")]:
         variants.append((a, a, base_mats))
     info = base_mats[0].info()
 
@@ -95,13 +98,9 @@ def main():
     for rnd in range(args.rounds):
         for name, algo, mats in variants:
             os.environ.pop("SM_XBAND_ABLATE", None)
-            os.environ.pop("SM_XBAND_OPT", None)
             if isinstance(algo, tuple):
-                algo, abl, opt = algo
-                if abl:
-                    os.environ["SM_XBAND_ABLATE"] = str(abl)
-                if opt is not None:
-                    os.environ["SM_XBAND_OPT"] = str(opt)
+                algo, abl = algo
+                os.environ["SM_XBAND_ABLATE"] = str(abl)
             for i in range(3):
                 d = data[i % len(data)]
                 mats[i % len(mats)].spmv(d[4], d[5], 1.0, 0.5, algo=algo)
