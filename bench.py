@@ -3,7 +3,8 @@
 
 Default (N=1): BASELINE config 2 -- B is 2^20 x 2^20 with exactly 16 distinct
 uniformly random columns per row (fp32 values from a 255-entry codebook),
-y = B x + 0.5 y with the stream kernel.  A step is one SpMV over one matrix.
+y = B x + 0.5 y with the library's AUTO path (the blocked column-band kernel
++ slab combine).  A step is one SpMV over one matrix.
 To measure HBM rather than the 256 MiB Infinity Cache, steps rotate over
 `--replicas` independent copies (matrix, x, y): 4 x 151 MB per rank.
 
@@ -15,9 +16,10 @@ ranks' algorithmic bytes divided by the max-over-ranks step time.
 Algorithmic bytes per SpMV: 8*nnz + 4*(rows+1) + 4*cols + 8*rows.
 
 Also reported, on the same JSON line:
-  roofline      the SpMV kernel alone: algorithmic bytes / mean kernel time
-                (HIP events around each launch on the launch stream) vs 8 TB/s;
-                `traffic` from rocprofv3 PMC (profiles/) when available.
+  roofline      the SpMV alone: algorithmic bytes / mean SpMV time (HIP events
+                around each sm_spmv call on its stream: the band kernel and, for
+                the blocked layout, the slab combine) vs 8 TB/s; `traffic` from
+                rocprofv3 PMC (profiles/traffic_<workload>_<layout>.json).
   cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C, 1 thread)
                 on the same matrix, ~10 s of CPU work.
   spmm          config 3 (same matrix, N=32 right-hand sides), GFLOP/s.
@@ -58,9 +60,15 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch measured by rocprofv3 PMC (tools/pmc_traffic.py)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked"}
+KERNELS = {"stream": "spmv_stream_kernel",
+           "exact": "spmv_xband_kernel (exact band layout)",
+           "blocked": "spmv_xband_kernel (blocked band layout) + combine_slabs_kernel"}
+
+
+def load_traffic(workload: str, layout: str):
+    """HBM bytes per SpMV measured by rocprofv3 PMC (tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{workload}_{layout}.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -76,7 +84,7 @@ def main():
     ap.add_argument("--rows-per-rank", type=int, default=1 << 20)
     ap.add_argument("--per-row", type=int, default=16)
     ap.add_argument("--replicas", type=int, default=4)
-    ap.add_argument("--algo", default="stream")
+    ap.add_argument("--algo", default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
@@ -156,10 +164,13 @@ def main():
     kmed = float(np.median(kern_ms))
     achieved = bytes_rank / (kmean * 1e-3) / 1e9
     workload = f"spmv_{R}x{C}_{per}_per_row"
-    traffic = load_traffic(workload) if world == 1 else None
+    info = reps[0]["M"].info()
+    layout = LAYOUTS[info["has_xband"]] if args.algo in ("auto", "xband") else "stream"
+    traffic = load_traffic(workload, layout) if world == 1 else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-            "traffic": traffic, "kernel": "spmv_stream_kernel",
+            "traffic": traffic, "kernel": KERNELS[layout], "layout": layout,
+            "xband_slabs": info["xband_slabs"], "xband_block_rows": info["xband_block_rows"],
             "kernel_ms_mean": round(kmean, 5), "kernel_ms_median": round(kmed, 5),
             "alg_bytes_per_launch": bytes_rank}
 
@@ -203,7 +214,7 @@ def main():
         y0 = r0["y"].cpu().numpy()
         oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)          # warm
         n_rep, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds and n_rep < 200:
+        while t_cpu < args.cpu_seconds and n_rep < 5000:
             c0 = time.perf_counter()
             oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)
             t_cpu += time.perf_counter() - c0

@@ -41,11 +41,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 
+// One asm statement naming every value: all of them are materialised (one
+// s_waitcnt) before anything after it, so hipcc cannot sink a read below a later
+// write it might alias (it would re-read after that write: one LDS round trip per
+// chunk instead of one per band).
+template <int N>
+__device__ __forceinline__ void pin_all(float *a, float *b) {
+    if constexpr (N == 1) {
+        asm volatile("" : "+v"(a[0]), "+v"(b[0]));
+    } else if constexpr (N == 2) {
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+    } else {
+        static_assert(N == 4, "CAP of 1, 2 or 4");
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
+                     "+v"(b[2]), "+v"(b[3]));
+    }
+}
+
 // ABL (ablation, development only, SM_XBAND_ABLATE): bit 1 skips the apply, bit 2
 // the x slice loads, bit 4 the entry loads, bit 16 the per-band barrier; the staged
-// slices are kept live so nothing upstream is dead-code removed.  Timing only:
-// results are wrong.
-template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL = 0>
+// slices are kept live so nothing upstream is dead-code removed.  Bit 32 records
+// s_memtime stamps (tile 0, 6 per band per wave, bands < 32) into y[0, 3072).
+// Timing only: results are wrong.
+// XR: x slices held in registers (2 or 4): slice p+XR+(XR==2) is loaded at band p and
+// stored XR-1+(XR==2) bands later -- a deeper ring hides more L2 latency per band.
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int XR, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
     int32_t slab_bands, const int32_t *__restrict__ chunk_start,
@@ -62,6 +82,8 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     constexpr int kWaves = THREADS / 64;
     constexpr int kXv = BAND / (4 * THREADS);   // float4 per thread per band
     static_assert(kXv >= 1, "band too small for the workgroup");
+    static_assert(XR == 2 || XR == 4, "x ring of 2 or 4 slices");
+    constexpr int kXAhead = XR == 4 ? 4 : 3;    // slice loaded at band p: p + kXAhead
     __shared__ __attribute__((aligned(16))) float xs[2][BAND];
     __shared__ float yacc[BROWS];
     const int tid = threadIdx.x;
@@ -114,7 +136,11 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         for (int k = 0; k < kXv; ++k)
             *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * THREADS)]) = xr[k];
     };
-    // Chunk c of band p for this wave (c beyond the band -> dummy after the load).
+    // Chunk c of band p for this wave.  A slot beyond the band's last chunk
+    // loads from past the descriptor's range (no memory request, reads 0): words
+    // are stored XOR the dummy word, so it is a dummy entry without a select
+    // (a select right after the load makes hipcc wait for it there -- at the
+    // loop's back edge -- instead of three bands later at the use).
     auto load_entries = [&](int32_t p, uint32_t *w, float *v) {
         const bool inb = p < nb;
         const int32_t c0 = inb ? cs_at(p) : 0;
@@ -122,20 +148,21 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
             const int32_t c = c0 + wave + k * kWaves;
-            const uint32_t off = 4u * (uint32_t)(c * 64 + lane);
-            uint32_t wl = (uint32_t)(lane * 131) & kColMask, vl = off;
+            const uint32_t off = c < c1 ? 4u * (uint32_t)(c * 64 + lane) : 0xFFFFFF00u;
+            uint32_t wl = ((uint32_t)(lane * 131) & kColMask) ^ kDummyWord, vl = off;
             if (!(ABL & 4)) {
                 wl = __builtin_amdgcn_raw_buffer_load_b32(w_src, off, 0, kAuxNt);
                 vl = __builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, kAuxNt);
             }
-            w[k] = c < c1 ? wl : kDummyWord;
+            w[k] = wl;
             v[k] = __uint_as_float(vl);
         }
     };
     // All chunks of a band at once: every lane's x and round-0 accumulator reads
     // issue together (one LDS wait), rank-0 terms land, then the few lanes of
-    // rank >= 1 re-read and add in rank order (program order within the wave;
-    // chunks of one band never share a row across waves).
+    // rank >= 1 re-read and add in rank order (program order within the wave).
+    // A row's segment lies in one chunk, so the chunks of a band -- this wave's
+    // and every other wave's -- touch disjoint rows.
     auto apply_band = [&](const float *xb, const uint32_t *wa, const float *va) {
         float xv[CAP], yv[CAP];
         uint32_t rk[CAP], rl[CAP];
@@ -143,14 +170,16 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         bool more = false;
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
-            rk[k] = (wa[k] >> kBits.col) & kRankMask;
+            const uint32_t wd = wa[k] ^ kDummyWord;
+            rk[k] = (wd >> kBits.col) & kRankMask;
             live[k] = rk[k] != kDummyRank;
-            const uint32_t cl = live[k] ? (wa[k] & kColMask) : 0u;
-            rl[k] = live[k] ? wa[k] >> (kBits.col + kBits.rank) : 0u;
+            const uint32_t cl = live[k] ? (wd & kColMask) : 0u;
+            rl[k] = live[k] ? wd >> (kBits.col + kBits.rank) : 0u;
             xv[k] = xb[cl];
             yv[k] = yacc[rl[k]];
             more |= live[k] && rk[k] > 0;
         }
+        pin_all<CAP>(xv, yv);
         float t[CAP];
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
@@ -172,12 +201,15 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 
     // Register rings with static roles (the band loop is unrolled by 4, so no
     // register ever moves -- a move would make hipcc wait for the load that
-    // filled it): x slices in X0/X1 (slice q lives in X[q % 2]), entries in
-    // E0..E3 (band q in E[q % 4]).
-    float4 X0[kXv], X1[kXv];
+    // filled it): x slice q lives in X[q % XR], the entries of band q in
+    // W/V[q % 4].
+    float4 X0[kXv], X1[kXv], X2[XR == 4 ? kXv : 1], X3[XR == 4 ? kXv : 1];
     uint32_t W0[CAP], W1[CAP], W2[CAP], W3[CAP];
     float V0[CAP], V1[CAP], V2[CAP], V3[CAP];
-    load_slice(0, X0);
+    // Accumulators first: this loop's own loads are drained before the pipeline
+    // starts.  Then the prologue issues its loads in exactly the order the loop
+    // leaves them pending at its back edge, so hipcc's vmcnt bookkeeping merges
+    // the two paths into the loop header without falling back to tighter waits.
     for (int32_t i = tid; i < nr; i += THREADS) {
         float v = 0.0f;
         if (slab == 0) {
@@ -186,25 +218,53 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         }
         yacc[i] = v;
     }
-    load_entries(0, W0, V0);
-    load_entries(1, W1, V1);
-    load_entries(2, W2, V2);
-    store_slice(0, X0);
-    load_slice(1, X1);
-    load_slice(2, X0);
+    if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
+        load_slice(0, X0);
+        load_slice(1, X1);
+        load_entries(0, W0, V0);
+        load_slice(2, X2);
+        load_entries(1, W1, V1);
+        load_slice(3, X3);
+        load_entries(2, W2, V2);
+        store_slice(0, X0);
+    } else {                   // pending after: E0 X1 E1 X0 E2
+        load_slice(0, X0);
+        load_entries(0, W0, V0);
+        load_slice(1, X1);
+        load_entries(1, W1, V1);
+        store_slice(0, X0);
+        load_slice(2, X0);
+        load_entries(2, W2, V2);
+    }
     __syncthreads();
 
-    // Band p: buffer p&1 holds slice p (visible); X[(p+1)%2] holds slice p+1.
-    // One barrier per band: the stores of slice p+1 into buffer (p+1)&1 (freed
-    // by the previous barrier) and this band's reads of buffer p&1 both finish
-    // before it.  Slice p+3 reuses the register set just stored; entries of
-    // band p+3 reuse the set of band p-1.  Loads past the tile's last band read
-    // the next slab's data or zeros (range-checked descriptors) and are never applied.
-    auto step = [&](int32_t p, float4 *xnext, uint32_t *wa, float *va, uint32_t *wl, float *vl) {
+    // Band p: buffer p&1 holds slice p (visible); the ring holds slice p+1.  One
+    // barrier per band: the stores of slice p+1 into buffer (p+1)&1 (freed by the
+    // previous barrier) and this band's reads of buffer p&1 both finish before
+    // it.  Slice p+kXAhead goes to the ring slot freed last (XR == 4: slice p's,
+    // stored a band ago; XR == 2: slice p+1's, stored just now); entries of band
+    // p+3 reuse the set of band p-1.  Loads past the tile's last band read the
+    // next slab's data or zeros (range-checked descriptors) and are never applied.
+    const bool tracing = (ABL & 32) && blockIdx.x == 0;
+    auto stamp = [&](int32_t p, int k) {
+        if (!tracing || p >= 32) return;
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (lane == 0) reinterpret_cast<uint32_t *>(y)[wave * 192 + p * 6 + k] = (uint32_t)t;
+    };
+    auto step = [&](int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va, uint32_t *wl,
+                    float *vl) {
+        stamp(p, 0);
         if (p + 4 >= cw + 128) load_cs_window(p);   // every 124 bands (nb > 124 only)
-        store_slice((p + 1) & 1, xnext);
-        load_slice(p + 3, xnext);
+        store_slice((p + 1) & 1, xst);
+        stamp(p, 1);
+        load_slice(p + kXAhead, xld);
         load_entries(p + 3, wl, vl);
+        stamp(p, 2);
+        if (tracing) {
+#pragma unroll
+            for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+            stamp(p, 3);
+        }
         // Every chunk of the band is in registers: the builder guarantees at
         // most CAP chunks per wave per band (no loop of loads in the pipeline,
         // so hipcc can count vmcnt exactly).
@@ -214,18 +274,30 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         } else {
             apply_band(xs[p & 1], wa, va);
         }
+        stamp(p, 4);
         if (!(ABL & 16)) __syncthreads();
+        stamp(p, 5);
     };
-    for (int32_t p = 0; p < nb; p += 4) {
-        step(p, X1, W0, V0, W3, V3);
-        if (p + 1 >= nb) break;
-        step(p + 1, X0, W1, V1, W0, V0);
-        if (p + 2 >= nb) break;
-        step(p + 2, X1, W2, V2, W1, V1);
-        if (p + 3 >= nb) break;
-        step(p + 3, X0, W3, V3, W2, V2);
+    // Whole groups of 4 bands, no early exit: a break out of the unrolled body
+    // would share the loop latch and make hipcc's vmcnt bookkeeping merge the
+    // break paths into the loop header (tight waits in the first step).  Steps
+    // past the tile's last band see only dummy entries and apply nothing.
+    const int32_t nb4 = (nb + 3) & ~3;
+    for (int32_t p = 0; p < nb4; p += 4) {
+        if constexpr (XR == 4) {
+            step(p, X1, X0, W0, V0, W3, V3);
+            step(p + 1, X2, X1, W1, V1, W0, V0);
+            step(p + 2, X3, X2, W2, V2, W1, V1);
+            step(p + 3, X0, X3, W3, V3, W2, V2);
+        } else {
+            step(p, X1, X1, W0, V0, W3, V3);
+            step(p + 1, X0, X0, W1, V1, W0, V0);
+            step(p + 2, X1, X1, W2, V2, W1, V1);
+            step(p + 3, X0, X0, W3, V3, W2, V2);
+        }
     }
-    for (int32_t i = tid; i < nr; i += THREADS) out[i] = yacc[i];
+    if (!tracing)
+        for (int32_t i = tid; i < nr; i += THREADS) out[i] = yacc[i];
     if (ABL && beta == -12345.0f) y[tid] = xs[0][tid] + xs[1][tid];   // keep the staging live
 }
 
@@ -243,7 +315,10 @@ __global__ __launch_bounds__(256) void combine_slabs_kernel(int32_t n_rows, int3
 template <int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
 hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                         float *y, float alpha, float beta, hipStream_t s) {
-    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, ABL>),
+    // x ring depth: 4 slices when a slice is 2 float4 per thread (blocked), 2 when
+    // it is 4 (exact: a deeper ring would not fit 128 VGPRs).
+    constexpr int XR = (1 << BAND_LOG2) / (4 * kXbThreads) <= 2 ? 4 : 2;
+    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),
                        dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s,
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,
                        xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, alpha, beta);
@@ -258,13 +333,15 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
     const char *abl_env = getenv("SM_XBAND_ABLATE");   // development only
     const int abl = abl_env ? atoi(abl_env) : 0;
     if (abl) {
-        if (cap > 2) return hipErrorInvalidValue;
+        if (cap > kXbMaxCap) return hipErrorInvalidValue;
         switch (abl) {
-        case 1: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 2: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 4: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 5: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 16: return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 1: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 2: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 4: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 5: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 16: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 32: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 32>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 37: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         default: return hipErrorInvalidValue;
         }
     }
@@ -293,7 +370,8 @@ hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         e = launch_kind<kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     else
         return hipErrorInvalidValue;
-    if (e != hipSuccess || xb.n_slabs == 1) return e;
+    const char *abl_env = getenv("SM_XBAND_ABLATE");   // development: a trace lives in y
+    if (e != hipSuccess || xb.n_slabs == 1 || (abl_env && (atoi(abl_env) & 32))) return e;
     hipLaunchKernelGGL(combine_slabs_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
                        n_rows, xb.n_slabs - 1, (const float *)xb.d_partials, y);
     return hipGetLastError();

@@ -20,7 +20,9 @@
 // the reference's order (bit-identical results, no atomics).
 //
 // Entry word: column in band | rank (all ones = dummy) | row in block, with
-// field widths from XbBits (xband.h).  Values are stored beside it (fp32).
+// field widths from XbBits (xband.h), stored XOR bits.dummy_word() so that a
+// zero word -- padding, or a load the kernel sends past its buffer's range --
+// decodes as a dummy.  Values are stored beside it (fp32).
 // chunk_start[b*nb + p] indexes the first chunk of (b, p); chunk_start[nblk*nb]
 // = total chunks.
 #include <algorithm>
@@ -128,7 +130,7 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
         out.too_dense = true;
         return false;
     }
-    out.word.assign((size_t)(total * 64), bits.dummy_word());
+    out.word.assign((size_t)(total * 64), 0u);   // dummies (stored XOR dummy_word)
     out.val.assign((size_t)(total * 64), 0.0f);
 
     for_blocks([&](int64_t b) {
@@ -143,8 +145,9 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
             for (int32_t k = 0; k < len; k++) {
                 const int64_t slot = chunk[p] * 64 + fill[p] + k;
                 const uint32_t cb = (uint32_t)(col[s + k] - p * band_cols);
-                out.word[(size_t)slot] = cb | ((uint32_t)k << bits.col) |
-                                         ((uint32_t)rl << (bits.col + bits.rank));
+                out.word[(size_t)slot] = (cb | ((uint32_t)k << bits.col) |
+                                          ((uint32_t)rl << (bits.col + bits.rank))) ^
+                                         bits.dummy_word();
                 out.val[(size_t)slot] = val[s + k];
             }
             fill[p] += len;

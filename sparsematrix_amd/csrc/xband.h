@@ -8,7 +8,7 @@ namespace smamd {
 
 // Entry word: bits [0, C) column in band, [C, C+K) rank inside the row's segment
 // (all ones = dummy), [C+K, 32) row in block; C = log2(band_cols), R = log2(max
-// block height), K = 32 - C - R.
+// block height), K = 32 - C - R.  Stored XOR dummy_word(): zero is a dummy.
 struct XbBits {
     int col, rank, row;
     constexpr uint32_t dummy_rank() const { return (1u << rank) - 1u; }
@@ -40,7 +40,7 @@ struct XbandHost {
     int64_t max_chunks_per_band = 0;
     bool too_dense = false;                    // a band exceeded the register capacity
     std::vector<int64_t> chunk_start;          // n_blocks * n_bands + 1
-    std::vector<uint32_t> word;                // 64 per chunk
+    std::vector<uint32_t> word;                // 64 per chunk, XOR bits.dummy_word()
     std::vector<float> val;
 };
 

@@ -10,9 +10,10 @@ cd /tmp || exit 1
 CMD="python3 $ROOT/tools/spmv_sweep.py --tiles 4096 --algos ${ALGO:-xband} --replicas 2 --rounds 1 --reps 4"
 G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
 G2="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE"
+G3="SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_ANY"
 i=0
-for g in "$G1" "$G2"; do
+for g in "$G1" "$G2" "$G3"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $g --kernel-trace --output-format csv -d "$OUT/g$i" -o run -- $CMD > "$OUT/g$i.log" 2>&1 || { tail -20 "$OUT/g$i.log"; exit 31; }
 done
-echo "pmc_kernel done"
+python3 "$ROOT/tools/pmc_summary.py" "$OUT"

@@ -9,7 +9,11 @@ applied to the kernel's FETCH_SIZE; WRITE_SIZE is used as is.  Caveat kept in
 the output: the SpMV kernel also issues 4-byte gathers (x) whose FETCH_SIZE
 calibration is not established; the figure is the wide-stream-corrected one.
 
-  python tools/pmc_traffic.py gpurun_out/pmc <kernel-substring> <workload> [alg_bytes]
+  python tools/pmc_traffic.py gpurun_out/pmc <kernel-substring[,substring...]> <workload> \
+      <layout> [alg_bytes]
+
+One SpMV may be several kernels (the blocked band layout: the band kernel and the
+slab combine): their per-dispatch averages are summed.
 """
 from __future__ import annotations
 
@@ -22,14 +26,21 @@ from collections import defaultdict
 csv.field_size_limit(1 << 30)
 
 
-def per_dispatch(path: str, kernel_sub: str) -> dict[str, float]:
-    vals = defaultdict(list)
-    with open(path, newline="") as f:
-        for row in csv.DictReader(f):
-            if kernel_sub in row["Kernel_Name"]:
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items() if v} | {
-        "_dispatches": max((len(v) for v in vals.values()), default=0)}
+def per_dispatch(path: str, kernel_subs: str) -> dict[str, float]:
+    """Per-dispatch average of each counter, summed over the listed kernels."""
+    out: dict[str, float] = defaultdict(float)
+    n = 0
+    for sub in kernel_subs.split(","):
+        vals = defaultdict(list)
+        with open(path, newline="") as f:
+            for row in csv.DictReader(f):
+                if sub in row["Kernel_Name"]:
+                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        for k, v in vals.items():
+            if v:
+                out[k] += sum(v) / len(v)
+        n = max([n] + [len(v) for v in vals.values()])
+    return dict(out) | {"_dispatches": n}
 
 
 def find(base: str, tag: str) -> str:
@@ -42,8 +53,8 @@ def find(base: str, tag: str) -> str:
 
 
 def main():
-    base, ksub, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-    alg = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    base, ksub, workload, layout = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
+    alg = int(sys.argv[5]) if len(sys.argv) > 5 else None
     fetch = per_dispatch(find(base, "bench_FETCH_SIZE"), ksub)
     write = per_dispatch(find(base, "bench_WRITE_SIZE"), ksub)
     hitmiss = per_dispatch(find(base, "bench_TCC_HIT_sum_TCC_MISS_sum"), ksub)
@@ -56,17 +67,20 @@ def main():
     hit = hitmiss.get("TCC_HIT_sum", 0.0)
     miss = hitmiss.get("TCC_MISS_sum", 0.0)
     out = {
-        "workload": workload, "kernel": ksub, "dispatches": fetch["_dispatches"],
+        "workload": workload, "layout": layout, "kernels": ksub.split(","),
+        "dispatches": fetch["_dispatches"],
         "fetch_size_bytes_raw": fetch_b, "write_size_bytes": write_b,
         "fetch_correction_factor": round(factor, 4),
         "calibration": "microbench read_kernel, 1 GiB float4 stream: FETCH_SIZE*1024*factor = 1 GiB",
         "hbm_bytes_per_launch": round(hbm), "alg_bytes_per_launch": alg,
         "traffic_over_alg": round(hbm / alg, 3) if alg else None,
         "l2_hit_rate": round(hit / (hit + miss), 4) if hit + miss else None,
-        "note": "x gathers are 4-byte accesses; their FETCH_SIZE calibration is not established",
+        "note": ("x gathers are 4-byte accesses; their FETCH_SIZE calibration is not established"
+                 if layout == "stream" else
+                 "x is read in wide 16-byte slices (the calibrated access width)"),
     }
     dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                       f"traffic_{workload}.json")
+                       f"traffic_{workload}_{layout}.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
