@@ -81,6 +81,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.xb.d_word);
     (void)hipFree(m->plan.xb.d_val);
     (void)hipFree(m->plan.xb.d_partials);
+    (void)hipFree(m->plan.xb.d_tickets);
     m->d_row_ptr = m->d_col = nullptr;
     m->d_val = nullptr;
     m->plan = Plan();
@@ -157,8 +158,12 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, (int64_t)cs32.size(), m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_word, (int64_t)xh.word.size(), m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_val, (int64_t)xh.val.size(), m->device_bytes));
-    if (n_slabs > 1)
-        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(n_slabs - 1) * m->n_rows, m->device_bytes));
+    if (n_slabs > 1) {
+        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
+        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(n_slabs - 1) * ps, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_tickets, xh.n_blocks, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)xh.n_blocks * sizeof(int32_t)));
+    }
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, cs32.data(), cs32.size() * 4, hipMemcpyHostToDevice));
     if (!xh.word.empty()) {
         SM_TRY_HIP(hipMemcpy(d.d_word, xh.word.data(), xh.word.size() * 4, hipMemcpyHostToDevice));

@@ -12,8 +12,12 @@
 // column order (bands ascend, ranks ascend inside a band).
 //
 // Slab 0 starts from beta*y and writes y; slab s > 0 starts from 0 and writes
-// partials[s-1]; combine_slabs_kernel then adds the partials to y in slab
-// order.  With one slab (the "exact" layout) every row is summed exactly in the
+// partials[s-1].  The last tile of a row block to finish (a ticket counter per
+// block) adds the partials to y in slab order -- the same sum whichever tile
+// finishes last.  The hand-off crosses CUs and XCDs: the slab sums are stored
+// write-through (sc1) and drained before the ticket, and the last tile reads
+// every one of them with sc1 loads (cdna_hip_programming.md §6 Guideline 16).
+// With one slab (the "exact" layout) every row is summed exactly in the
 // reference's order: bit-identical.  Layout and builder: xband.h / xband.cpp.
 //
 // Why x goes through LDS (profiles/r01_microbench.txt): random 4-byte gathers
@@ -40,6 +44,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
                                              0x00020000);
 }
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
+constexpr int kAuxSc1 = 16; // write-through store / L1-bypassing load (cross-CU hand-off)
 
 // One asm statement naming every value: all of them are materialised (one
 // s_waitcnt) before anything after it, so hipcc cannot sink a read below a later
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     int32_t slab_bands, const int32_t *__restrict__ chunk_start,
     const uint32_t *__restrict__ word, const float *__restrict__ val,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
-    float alpha, float beta) {
+    int32_t *__restrict__ tickets, float alpha, float beta) {
     constexpr int BAND = 1 << BAND_LOG2;
     constexpr int BROWS = 1 << ROWS_LOG2;
     constexpr XbBits kBits = xb_bits(BAND_LOG2, ROWS_LOG2);
@@ -104,7 +109,6 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         rsrc(word + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
     const __amdgpu_buffer_rsrc_t v_src =
         rsrc(val + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
-    float *out = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * n_rows + r0;
     // Chunk table window in registers: lane l holds cs[cw + l] and cs[cw + 64 + l]
     // (tile-relative); scalar reads via readlane, reloaded every 124 bands.
     int32_t cw = 0;
@@ -296,20 +300,95 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             step(p + 3, X0, X0, W3, V3, W2, V2);
         }
     }
-    if (!tracing)
-        for (int32_t i = tid; i < nr; i += THREADS) out[i] = yacc[i];
+    if (tracing) return;
+    if (n_slabs == 1) {
+        for (int32_t i = tid; i < nr; i += THREADS) y[r0 + i] = yacc[i];
+    } else {
+        // Publish this slab's sums (write-through, float4 where the rows allow),
+        // then take a ticket.  Partials sit at a 4-aligned stride (ps).
+        const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
+        float *outp = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * ps + r0;
+        const bool vec = ((uintptr_t)(y + r0) & 15) == 0;   // partials are always aligned
+        const int32_t nr4 = vec ? (nr & ~3) : 0;
+        const bool vec_out = slab != 0 || vec;
+        const int32_t no4 = vec_out ? (nr & ~3) : 0;
+        const __amdgpu_buffer_rsrc_t o_src = rsrc(outp, (uint64_t)nr * 4);
+        for (int32_t i = 4 * tid; i < no4; i += 4 * THREADS) {
+            const float4 v = *reinterpret_cast<const float4 *>(&yacc[i]);
+            const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                             __float_as_uint(v.w)};
+            __builtin_amdgcn_raw_buffer_store_b128(u, o_src, 4u * i, 0, kAuxSc1);
+        }
+        for (int32_t i = no4 + tid; i < nr; i += THREADS)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yacc[i]), o_src, 4u * i, 0,
+                                                  kAuxSc1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int32_t t = __hip_atomic_fetch_add(tickets + b, 1, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+            xs[0][0] = __int_as_float(t);   // broadcast through the x buffer (no longer read)
+        }
+        __syncthreads();
+        if (__float_as_int(xs[0][0]) == n_slabs - 1) {
+            // Last tile of the block: every other slab has published.  y (slab 0)
+            // plus the partials in slab order, every read an sc1 load; each thread
+            // keeps its rows' loads of up to 4 slabs in flight at once.
+            constexpr int kQ = BROWS / (4 * THREADS);   // float4 rows per thread
+            const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
+            float4 acc[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const uint32_t off = 16u * (uint32_t)(tid + q * THREADS);
+                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(y_src, off, 0, kAuxSc1);
+                acc[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                     __uint_as_float(u.z), __uint_as_float(u.w));
+            }
+            for (int32_t s0 = 1; s0 < n_slabs; s0 += 4) {
+                u32x4 pv[4][kQ];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int32_t sl = min(s0 + j, n_slabs - 1);
+                    const __amdgpu_buffer_rsrc_t p_src =
+                        rsrc(partials + (int64_t)(sl - 1) * ps + r0, (uint64_t)nr * 4);
+#pragma unroll
+                    for (int q = 0; q < kQ; ++q)
+                        pv[j][q] = __builtin_amdgcn_raw_buffer_load_b128(
+                            p_src, 16u * (uint32_t)(tid + q * THREADS), 0, kAuxSc1);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (s0 + j >= n_slabs) break;
+#pragma unroll
+                    for (int q = 0; q < kQ; ++q) {
+                        acc[q].x = __fadd_rn(acc[q].x, __uint_as_float(pv[j][q].x));
+                        acc[q].y = __fadd_rn(acc[q].y, __uint_as_float(pv[j][q].y));
+                        acc[q].z = __fadd_rn(acc[q].z, __uint_as_float(pv[j][q].z));
+                        acc[q].w = __fadd_rn(acc[q].w, __uint_as_float(pv[j][q].w));
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int32_t i = 4 * (tid + q * THREADS);
+                if (i < nr4) *reinterpret_cast<float4 *>(y + r0 + i) = acc[q];
+            }
+            // Rows not covered above (a ragged last block, or y not 16-byte aligned).
+            for (int32_t i = nr4 + tid; i < nr; i += THREADS) {
+                float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(y_src, 4u * i, 0, kAuxSc1));
+                for (int32_t sl = 1; sl < n_slabs; ++sl) {
+                    const __amdgpu_buffer_rsrc_t p_src =
+                        rsrc(partials + (int64_t)(sl - 1) * ps + r0, (uint64_t)nr * 4);
+                    a = __fadd_rn(a, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                         p_src, 4u * i, 0, kAuxSc1)));
+                }
+                y[r0 + i] = a;
+            }
+            if (tid == 0)
+                __hip_atomic_store(tickets + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (ABL && beta == -12345.0f) y[tid] = xs[0][tid] + xs[1][tid];   // keep the staging live
-}
-
-// y[r] = (((y[r] + p_0[r]) + p_1[r]) + ...): the slab partial sums in slab order.
-__global__ __launch_bounds__(256) void combine_slabs_kernel(int32_t n_rows, int32_t n_parts,
-                                                            const float *__restrict__ partials,
-                                                            float *__restrict__ y) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= n_rows) return;
-    float acc = y[r];
-    for (int32_t s = 0; s < n_parts; ++s) acc = __fadd_rn(acc, partials[(int64_t)s * n_rows + r]);
-    y[r] = acc;
 }
 
 template <int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
@@ -321,7 +400,8 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
     hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),
                        dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s,
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,
-                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, alpha, beta);
+                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets,
+                       alpha, beta);
     return hipGetLastError();
 }
 
@@ -359,22 +439,16 @@ hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (xb.n_bands > kXbMaxBands || xb.n_slabs < 1 || xb.slab_bands < 1 ||
         (int64_t)xb.n_slabs * xb.slab_bands < xb.n_bands ||
         (int64_t)(xb.n_slabs - 1) * xb.slab_bands >= xb.n_bands ||
-        (xb.n_slabs > 1 && !xb.d_partials))
+        (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
         return hipErrorInvalidValue;
-    hipError_t e;
+    hipError_t e = hipErrorInvalidValue;
     if (xb.kind == kXbExact && xb.band_cols == 1 << kXbExactBandLog2 &&
         xb.block_rows <= 1 << kXbExactRowsLog2)
         e = launch_kind<kXbExactBandLog2, kXbExactRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     else if (xb.kind == kXbBlocked && xb.band_cols == 1 << kXbBlockedBandLog2 &&
              xb.block_rows <= 1 << kXbBlockedRowsLog2)
         e = launch_kind<kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    else
-        return hipErrorInvalidValue;
-    const char *abl_env = getenv("SM_XBAND_ABLATE");   // development: a trace lives in y
-    if (e != hipSuccess || xb.n_slabs == 1 || (abl_env && (atoi(abl_env) & 32))) return e;
-    hipLaunchKernelGGL(combine_slabs_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
-                       n_rows, xb.n_slabs - 1, (const float *)xb.d_partials, y);
-    return hipGetLastError();
+    return e;
 }
 
 }  // namespace smamd
