@@ -115,8 +115,11 @@ int32_t tile_nnz_setting() {
 }
 
 // Column-band layout.  Which one: SM_XBAND=0 disables it,
-// SM_XBAND=1 forces it; otherwise the blocked layout is built when sweeping x
-// through every tile's LDS costs less than the random gathers it replaces.
+// SM_XBAND=1 forces it; otherwise it is built when sweeping x through every
+// tile's LDS costs less than the random gathers it replaces.  Cost model from
+// profiles/r01_microbench.txt: a tile streams x into LDS at ~85 GB/s per CU
+// (~22 TB/s chip-wide) while 4-byte gathers run at 75-200 G/s by the size of x,
+// so the sweep wins while its bytes stay under ~20x the matrix's 8 B per term.
 // SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
 XbKind xband_kind_setting() {
     const char *e = getenv("SM_XBAND_KIND");
@@ -132,7 +135,7 @@ bool want_xband(const sm_matrix *m) {
     const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
     const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
     const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
-    return x_sweep <= 10.0 * stream && m->n_cols >= 8192;
+    return x_sweep <= 20.0 * stream && m->n_cols >= 8192;
 }
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {

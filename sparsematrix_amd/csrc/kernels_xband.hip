@@ -56,8 +56,10 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
         asm volatile("" : "+v"(a[0]), "+v"(b[0]));
     } else if constexpr (N == 2) {
         asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+    } else if constexpr (N == 3) {
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]));
     } else {
-        static_assert(N == 4, "CAP of 1, 2 or 4");
+        static_assert(N == 4, "CAP of 1 to 4");
         asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
                      "+v"(b[2]), "+v"(b[3]));
     }
@@ -427,6 +429,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
     }
     if (cap <= 1) return launch_tiles<BAND_LOG2, ROWS_LOG2, 1, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     if (cap <= 2) return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 3) return launch_tiles<BAND_LOG2, ROWS_LOG2, 3, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     if (cap <= kXbMaxCap) return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     return hipErrorInvalidValue;
 }

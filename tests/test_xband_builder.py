@@ -1,0 +1,25 @@
+"""Host logic of the column-band layout builder (sparsematrix_amd/csrc/xband.cpp),
+no GPU: tests/native/xband_asan.cpp is compiled with AddressSanitizer and run.
+It rebuilds every row from the layout (both the exact and the blocked bit layout)
+and checks order, ranks, register capacity and the dummy encoding."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_xband_builder_under_asan(tmp_path):
+    exe = tmp_path / "xband_asan"
+    src = [os.path.join(ROOT, "tests", "native", "xband_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "xband.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "xband_asan: ok" in r.stdout
