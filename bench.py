@@ -20,8 +20,9 @@ Also reported, on the same JSON line:
                 around each sm_spmv call on its stream: the band kernel and, for
                 the blocked layout, the slab combine) vs 8 TB/s; `traffic` from
                 rocprofv3 PMC (profiles/traffic_<workload>_<layout>.json).
-  cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C, 1 thread)
-                on the same matrix, ~10 s of CPU work.
+  cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C) on the same
+                matrix, over the box's CPU share (OpenMP, <= 16 threads; SURVEY
+                §8d B2) with the 1-thread figure inside; ~15 s of CPU work.
   spmm          config 3 (same matrix, N=32 right-hand sides), GFLOP/s.
 """
 from __future__ import annotations
@@ -212,18 +213,31 @@ def main():
         va = r0["va"].cpu().numpy()
         x = r0["x_full"].cpu().numpy()
         y0 = r0["y"].cpu().numpy()
-        oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)          # warm
-        n_rep, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds and n_rep < 5000:
-            c0 = time.perf_counter()
-            oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)
-            t_cpu += time.perf_counter() - c0
-            n_rep += 1
-        cpu = {"value": round(bytes_rank * n_rep / t_cpu / 1e9, 3), "unit": "GB/s", "cores": 1,
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
+
+        def timed(fn, budget):
+            fn()                                                # warm
+            n_rep, t_cpu = 0, 0.0
+            while t_cpu < budget and n_rep < 5000:
+                c0 = time.perf_counter()
+                fn()
+                t_cpu += time.perf_counter() - c0
+                n_rep += 1
+            return n_rep, t_cpu
+
+        n1, t1 = timed(lambda: oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5), args.cpu_seconds)
+        nm, tm = timed(lambda: oracle.csr_spmv_mt(rp, ci, va, x, y0, 1.0, 0.5, threads=threads),
+                       args.cpu_seconds / 2)
+        cpu = {"value": round(bytes_rank * nm / tm / 1e9, 3), "unit": "GB/s", "cores": threads,
                "kind": "port",
-               "sample": f"oracle same-order CSR SpMV (C, 1 thread) on the full config-2 matrix "
-                         f"(replica 0), {n_rep} reps in {t_cpu:.1f} s",
-               "ms_per_spmv": round(1e3 * t_cpu / n_rep, 3), "cpu": cpu_model(),
+               "sample": f"oracle same-order CSR SpMV (C, OpenMP over rows, {threads} threads) on "
+                         f"the full config-2 matrix (replica 0), {nm} reps in {tm:.1f} s",
+               "ms_per_spmv": round(1e3 * tm / nm, 3),
+               "single_thread": {"value": round(bytes_rank * n1 / t1 / 1e9, 3), "unit": "GB/s",
+                                 "cores": 1, "ms_per_spmv": round(1e3 * t1 / n1, 3),
+                                 "sample": f"{n1} reps in {t1:.1f} s (the reference kernel is "
+                                           f"single-threaded)"},
+               "cpu": cpu_model(),
                "nproc": os.cpu_count()}
 
     if rank == 0:

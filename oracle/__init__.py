@@ -68,6 +68,8 @@ def lib():
         L.om_csr_spmv.argtypes = [C.c_int64, _i64p, _i32p, _f32p, _f32p, _f32p, C.c_float, C.c_float]
         L.om_csr_spmv_i32.argtypes = [C.c_int64, _i32p, _i32p, _f32p, _f32p, _f32p, C.c_float,
                                       C.c_float]
+        L.om_csr_spmv_i32_mt.argtypes = [C.c_int64, _i32p, _i32p, _f32p, _f32p, _f32p, C.c_float,
+                                         C.c_float, C.c_int32]
         L.om_csr_spmm.argtypes = [C.c_int64, _i64p, _i32p, _f32p, C.c_int32, _f32p, C.c_int64,
                                   _f32p, C.c_int64, C.c_float, C.c_float]
         L.om_csr_spmv_f64.argtypes = [C.c_int64, _i64p, _i32p, _f32p, _f32p, _f32p, _f64p, _f64p,
@@ -184,6 +186,18 @@ def csr_spmv(row_ptr, col_idx, val, x, y, alpha=1.0, beta=1.0) -> np.ndarray:
     else:
         lib().om_csr_spmv(n, row_ptr.astype(np.int64), _nz1(col_idx, np.int32),
                           _nz1(val, np.float32), _nz1(x, np.float32), out, alpha, beta)
+    return out
+
+
+def csr_spmv_mt(row_ptr, col_idx, val, x, y, alpha=1.0, beta=1.0, threads=1) -> np.ndarray:
+    """csr_spmv with the rows split over `threads` OpenMP threads (int32 row_ptr);
+    bit-identical to csr_spmv (each row is still summed in order by one thread)."""
+    row_ptr = np.ascontiguousarray(row_ptr, np.int32)
+    out = np.array(y, np.float32, copy=True).reshape(-1)
+    n = row_ptr.shape[0] - 1
+    if n > 0:
+        lib().om_csr_spmv_i32_mt(n, row_ptr, _nz1(col_idx, np.int32), _nz1(val, np.float32),
+                                 _nz1(x, np.float32), out, alpha, beta, int(threads))
     return out
 
 

@@ -246,6 +246,30 @@ void om_csr_spmv_i32(int64_t n_rows, const int32_t *row_ptr, const int32_t *col_
     CSR_SPMV_BODY(row_ptr)
 }
 
+/* The same kernel with the rows split over n_threads OpenMP threads (SURVEY §8d
+ * baseline B2, "all cores"): every row is still summed by one thread in the
+ * reference's order, so the result is bit-identical to om_csr_spmv_i32. */
+void om_csr_spmv_i32_mt(int64_t n_rows, const int32_t *row_ptr, const int32_t *col_idx,
+                        const float *val, const float *x, float *y, float alpha, float beta,
+                        int32_t n_threads) {
+#pragma omp parallel for schedule(static) num_threads(n_threads)
+    for (int64_t r0 = 0; r0 < n_rows; r0 += 4096) {
+        const int64_t r1 = r0 + 4096 < n_rows ? r0 + 4096 : n_rows;
+        for (int64_t r = r0; r < r1; r++) {
+            float acc = y[r];
+            if (beta != 1.0f) acc = acc * beta;
+            if (alpha != 0.0f) {
+                for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; e++) {
+                    const float v = val[e] * alpha;
+                    const float prod = x[col_idx[e]] * v;
+                    acc = acc + prod;
+                }
+            }
+            y[r] = acc;
+        }
+    }
+}
+
 void om_csr_spmm(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
                  const float *val, int32_t n_rhs, const float *X, int64_t ldx,
                  float *Y, int64_t ldy, float alpha, float beta) {

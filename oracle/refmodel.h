@@ -76,6 +76,9 @@ void om_csr_spmm(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
 /* Same as om_csr_spmv but with int32 row_ptr (the device format). */
 void om_csr_spmv_i32(int64_t n_rows, const int32_t *row_ptr, const int32_t *col_idx,
                      const float *val, const float *x, float *y, float alpha, float beta);
+void om_csr_spmv_i32_mt(int64_t n_rows, const int32_t *row_ptr, const int32_t *col_idx,
+                        const float *val, const float *x, float *y, float alpha, float beta,
+                        int32_t n_threads);
 
 /* fp64 reference and per-row sum of |terms| (for tolerance pins). */
 void om_csr_spmv_f64(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,

@@ -122,3 +122,18 @@ def test_restatement_vs_live_reference_random():
         al, be = float(rng.choice([1.0, 1.3, 0.0])), float(rng.choice([1.0, 0.7, 0.0]))
         assert bits_equal(ref.add_mat_mat(a, m, kk, cc, nn, al, be),
                           om.add_mat_mat(a, m, kk, cc, nn, al, be))
+
+
+def test_csr_spmv_multithread_bit_identical():
+    """The all-cores CPU baseline (OpenMP rows) sums every row in the same order."""
+    rng = np.random.default_rng(11)
+    n, per = 50000, 16
+    rp = np.arange(0, n * per + 1, per, dtype=np.int32)
+    ci = np.sort(rng.integers(0, n, (n, per)), 1).astype(np.int32).ravel()
+    va = rng.uniform(-1, 1, n * per).astype(np.float32)
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    y = rng.uniform(-1, 1, n).astype(np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y, 1.3, 0.7)
+    for t in (1, 3, 8):
+        got = oracle.csr_spmv_mt(rp, ci, va, x, y, 1.3, 0.7, threads=t)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), t
