@@ -164,11 +164,19 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             v[k] = __uint_as_float(vl);
         }
     };
-    // All chunks of a band at once: every lane's x and round-0 accumulator reads
-    // issue together (one LDS wait), rank-0 terms land, then the few lanes of
-    // rank >= 1 re-read and add in rank order (program order within the wave).
-    // A row's segment lies in one chunk, so the chunks of a band -- this wave's
-    // and every other wave's -- touch disjoint rows.
+    // All chunks of a band at once: every lane's x and accumulator reads issue
+    // together (one LDS wait).  A row's terms inside a band form one segment of
+    // consecutive lanes of one chunk (ranks 0, 1, ...); the segment's running sum
+    // moves up the lanes in registers (DPP wave_shr:1, one round per rank) and
+    // only its last lane writes the accumulator -- the terms still added one at a
+    // time in ascending column order.  Chunks of a band, in this wave and in every
+    // other wave, touch disjoint rows.
+    auto shr1 = [](float v) {   // lane i <- lane i-1 (lane 0 never has rank >= 1)
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+    };
+    auto shl1 = [](uint32_t v) {   // lane i <- lane i+1; lane 63 <- the dummy rank
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)kDummyRank, (int)v, 0x130, 0xF, 0xF, false);
+    };
     auto apply_band = [&](const float *xb, const uint32_t *wa, const float *va) {
         float xv[CAP], yv[CAP];
         uint32_t rk[CAP], rl[CAP];
@@ -186,22 +194,28 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             more |= live[k] && rk[k] > 0;
         }
         pin_all<CAP>(xv, yv);
-        float t[CAP];
+        float t[CAP], acc[CAP];
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
             t[k] = __fmul_rn(xv[k], __fmul_rn(va[k], alpha));
-            if (live[k] && rk[k] == 0) yacc[rl[k]] = __fadd_rn(yv[k], t[k]);
+            acc[k] = __fadd_rn(yv[k], t[k]);
         }
         if (__any(more)) {
             for (uint32_t r = 1;; ++r) {
                 bool again = false;
 #pragma unroll
                 for (int k = 0; k < CAP; ++k) {
-                    if (live[k] && rk[k] == r) yacc[rl[k]] = __fadd_rn(yacc[rl[k]], t[k]);
+                    const float prev = shr1(acc[k]);
+                    if (rk[k] == r) acc[k] = __fadd_rn(prev, t[k]);
                     again |= live[k] && rk[k] > r;
                 }
                 if (!__any(again)) break;
             }
+        }
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
+            if (last) yacc[rl[k]] = acc[k];
         }
     };
 
