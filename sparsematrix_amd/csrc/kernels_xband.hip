@@ -92,7 +92,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     static_assert(XR == 2 || XR == 4, "x ring of 2 or 4 slices");
     constexpr int kXAhead = XR == 4 ? 4 : 3;    // slice loaded at band p: p + kXAhead
     __shared__ __attribute__((aligned(16))) float xs[2][BAND];
-    __shared__ float yacc[BROWS];
+    __shared__ float yacc[BROWS + 64];   // + one scratch slot per lane (writes that land nowhere)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -111,21 +111,24 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         rsrc(word + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
     const __amdgpu_buffer_rsrc_t v_src =
         rsrc(val + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
-    // Chunk table window in registers: lane l holds cs[cw + l] and cs[cw + 64 + l]
-    // (tile-relative); scalar reads via readlane, reloaded every 124 bands.
+    // Chunk table window in registers: lane l holds cs[cw + l] (lo) and
+    // cs[cw + 64 + l] (hi), tile-relative; read by readlane with a branch-free
+    // select.  Every 64 bands the window advances: hi (loaded 64 bands earlier)
+    // becomes lo and the next hi is prefetched -- no load is waited for at once.
     int32_t cw = 0;
-    int32_t cs_lo = 0, cs_hi = 0;
-    auto load_cs_window = [&](int32_t base) {
-        cw = base;
-        const int32_t i0 = min(base + lane, nb), i1 = min(base + 64 + lane, nb);
-        cs_lo = csg[i0] - c_first;
-        cs_hi = csg[i1] - c_first;
+    int32_t cs_lo = csg[min(lane, nb)] - c_first;
+    int32_t cs_hi = csg[min(64 + lane, nb)] - c_first;
+    auto advance_cs_window = [&]() {
+        cw += 64;
+        cs_lo = cs_hi;
+        cs_hi = csg[min(cw + 64 + lane, nb)] - c_first;
     };
     auto cs_at = [&](int32_t i) -> int32_t {   // i in [cw, cw + 128), wave-uniform
         const int32_t j = i - cw;
-        return j < 64 ? __builtin_amdgcn_readlane(cs_lo, j) : __builtin_amdgcn_readlane(cs_hi, j - 64);
+        const int32_t lo = __builtin_amdgcn_readlane(cs_lo, j & 63);
+        const int32_t hi = __builtin_amdgcn_readlane(cs_hi, j & 63);
+        return j < 64 ? lo : hi;
     };
-    load_cs_window(0);
 
     auto load_slice = [&](int32_t p, float4 *xr) {
 #pragma unroll
@@ -187,9 +190,8 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             const uint32_t wd = wa[k] ^ kDummyWord;
             rk[k] = (wd >> kBits.col) & kRankMask;
             live[k] = rk[k] != kDummyRank;
-            const uint32_t cl = live[k] ? (wd & kColMask) : 0u;
-            rl[k] = live[k] ? wd >> (kBits.col + kBits.rank) : 0u;
-            xv[k] = xb[cl];
+            rl[k] = wd >> (kBits.col + kBits.rank);   // dummies decode to row 0, column 0
+            xv[k] = xb[wd & kColMask];
             yv[k] = yacc[rl[k]];
             more |= live[k] && rk[k] > 0;
         }
@@ -213,9 +215,9 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             }
         }
 #pragma unroll
-        for (int k = 0; k < CAP; ++k) {
+        for (int k = 0; k < CAP; ++k) {   // every lane writes: the segment's last to its row
             const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
-            if (last) yacc[rl[k]] = acc[k];
+            yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
         }
     };
 
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     auto step = [&](int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va, uint32_t *wl,
                     float *vl) {
         stamp(p, 0);
-        if (p + 4 >= cw + 128) load_cs_window(p);   // every 124 bands (nb > 124 only)
+        if (p + 3 >= cw + 64) advance_cs_window();   // this step reads cs[p+3], cs[p+4]
         store_slice((p + 1) & 1, xst);
         stamp(p, 1);
         load_slice(p + kXAhead, xld);
