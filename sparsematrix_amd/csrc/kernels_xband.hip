@@ -46,6 +46,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 constexpr int kAuxSc1 = 16; // write-through store / L1-bypassing load (cross-CU hand-off)
 
+// vmcnt retires in issue order: waiting until only the N most recent vector loads
+// are outstanding retires every older one, including LDS-DMA that hipcc does not count.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // One asm statement naming every value: all of them are materialised (one
 // s_waitcnt) before anything after it, so hipcc cannot sink a read below a later
 // write it might alias (it would re-read after that write: one LDS round trip per
@@ -67,11 +75,15 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
 
 // ABL (ablation, development only, SM_XBAND_ABLATE): bit 1 skips the apply, bit 2
 // the x slice loads, bit 4 the entry loads, bit 16 the per-band barrier; the staged
-// slices are kept live so nothing upstream is dead-code removed.  Bit 32 records
+// slices are kept live so nothing upstream is dead-code removed; bit 128 skips the
+// slice stores into LDS (the loaded values kept live), 256 the whole band loop, 512
+// the slab hand-off and combine (plain stores instead).  Bit 32 records
 // s_memtime stamps (tile 0, 6 per band per wave, bands < 32) into y[0, 3072).
 // Timing only: results are wrong.
 // XR: x slices held in registers (2 or 4): slice p+XR+(XR==2) is loaded at band p and
 // stored XR-1+(XR==2) bands later -- a deeper ring hides more L2 latency per band.
+// XR == 0: no register ring -- slices go HBM/L2 -> LDS directly (LDS-DMA) into a
+// ring of three LDS buffers, slice p+2 issued at band p.
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int XR, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
@@ -89,10 +101,13 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     constexpr int kWaves = THREADS / 64;
     constexpr int kXv = BAND / (4 * THREADS);   // float4 per thread per band
     static_assert(kXv >= 1, "band too small for the workgroup");
-    static_assert(XR == 2 || XR == 4, "x ring of 2 or 4 slices");
-    constexpr int kXAhead = XR == 4 ? 4 : 3;    // slice loaded at band p: p + kXAhead
-    __shared__ __attribute__((aligned(16))) float xs[2][BAND];
-    __shared__ float yacc[BROWS + 64];   // + one scratch slot per lane (writes that land nowhere)
+    static_assert(XR == 0 || XR == 2 || XR == 4, "x ring of 2 or 4 slices, or LDS-DMA");
+    constexpr bool kDma = XR == 0;
+    constexpr int kXAhead = XR == 4 ? 4 : 3;    // register ring: slice loaded at band p: p + kXAhead
+    constexpr int kXBufs = kDma ? 3 : 2;        // LDS x buffers
+    constexpr int kScratch = kDma ? 0 : 64;     // per-lane write slots (no room with 3 buffers)
+    __shared__ __attribute__((aligned(16))) float xs[kXBufs][BAND];
+    __shared__ float yacc[BROWS + kScratch];   // + one scratch slot per lane (writes that land nowhere)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -130,10 +145,13 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         return j < 64 ? lo : hi;
     };
 
+    // Slices past the tile's last band (the pipeline's run-out) load from past the
+    // descriptor's range: no memory request (they would be 4 bands of wasted x).
     auto load_slice = [&](int32_t p, float4 *xr) {
 #pragma unroll
         for (int k = 0; k < kXv; ++k) {
-            const uint32_t off = 4u * (uint32_t)(p * BAND + 4 * (tid + k * THREADS));
+            const uint32_t off = p < nb ? 4u * (uint32_t)(p * BAND + 4 * (tid + k * THREADS))
+                                        : 0xFFFFFFF0u;
             u32x4 v = {off, off, off, off};
             if (!(ABL & 2)) v = __builtin_amdgcn_raw_buffer_load_b128(xr_src, off, 0, 0);
             xr[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
@@ -142,8 +160,35 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     };
     auto store_slice = [&](int buf, const float4 *xr) {
 #pragma unroll
-        for (int k = 0; k < kXv; ++k)
-            *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * THREADS)]) = xr[k];
+        for (int k = 0; k < kXv; ++k) {
+            if (ABL & 128)
+                asm volatile("" ::"v"(xr[k].x), "v"(xr[k].y), "v"(xr[k].z), "v"(xr[k].w));
+            else
+                *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * THREADS)]) = xr[k];
+        }
+    };
+    // LDS-DMA of slice p into buffer `buf`: piece m (256 floats, 1 KiB) is
+    // wave-instruction k of wave m % 16.  Issued from asm so hipcc does not count
+    // it (a counted LDS-DMA makes hipcc drain vmcnt at every barrier and at every
+    // use of an ordinary load); wait_vmcnt retires it before the barrier.
+    const uint32_t xs_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) float *)&xs[0][0];
+    auto dma_slice = [&](int32_t p, int buf) {
+#pragma unroll
+        for (int k = 0; k < kXv; ++k) {
+            const int m = k * (THREADS / 64) + wave;
+            const uint32_t voff = p < nb && !(ABL & 2)
+                                      ? 4u * (uint32_t)(p * BAND + m * 256 + lane * 4)
+                                      : 0xFFFFFFF0u;
+            const uint32_t lds =
+                __builtin_amdgcn_readfirstlane(xs_lds + 4u * (uint32_t)(buf * BAND + m * 256));
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(xr_src), "s"(lds)
+                : "memory");
+        }
     };
     // Chunk c of band p for this wave.  A slot beyond the band's last chunk
     // loads from past the descriptor's range (no memory request, reads 0): words
@@ -217,7 +262,10 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {   // every lane writes: the segment's last to its row
             const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
-            yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
+            if constexpr (kScratch > 0)
+                yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
+            else if (last)
+                yacc[rl[k]] = acc[k];
         }
     };
 
@@ -232,15 +280,53 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // starts.  Then the prologue issues its loads in exactly the order the loop
     // leaves them pending at its back edge, so hipcc's vmcnt bookkeeping merges
     // the two paths into the loop header without falling back to tighter waits.
-    for (int32_t i = tid; i < nr; i += THREADS) {
-        float v = 0.0f;
-        if (slab == 0) {
-            v = y[r0 + i];
-            if (beta != 1.0f) v = __fmul_rn(v, beta);
+    // All of a thread's rows in flight at once (one 16-byte load per 4 rows when y
+    // is aligned, else one dword load per row; rows past nr read 0 and are never
+    // written back): a load-then-store loop would pay one memory latency per row.
+    constexpr int kQ = BROWS / (4 * THREADS);   // float4 rows per thread
+    const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
+    if (slab == 0) {
+        const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
+        float4 v[kQ];
+        if (y_vec) {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(
+                    yi_src, 16u * (uint32_t)(tid + q * THREADS), 0, 0);
+                v[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                   __uint_as_float(u.z), __uint_as_float(u.w));
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const uint32_t o = 16u * (uint32_t)(tid + q * THREADS);
+                v[q] = make_float4(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 4, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 8, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 12, 0, 0)));
+            }
         }
-        yacc[i] = v;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (beta != 1.0f)
+                v[q] = make_float4(__fmul_rn(v[q].x, beta), __fmul_rn(v[q].y, beta),
+                                   __fmul_rn(v[q].z, beta), __fmul_rn(v[q].w, beta));
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = v[q];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
+    if constexpr (kDma) {      // pending after: E1 D1 E2 (D0, E0 retired)
+        load_entries(0, W0, V0);
+        dma_slice(0, 0);
+        load_entries(1, W1, V1);
+        dma_slice(1, 1);
+        load_entries(2, W2, V2);
+        wait_vmcnt<4 * CAP + kXv>();   // slice 0 landed
+    } else if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
         load_slice(0, X0);
         load_slice(1, X1);
         load_entries(0, W0, V0);
@@ -277,9 +363,14 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
                     float *vl) {
         stamp(p, 0);
         if (p + 3 >= cw + 64) advance_cs_window();   // this step reads cs[p+3], cs[p+4]
-        store_slice((p + 1) & 1, xst);
-        stamp(p, 1);
-        load_slice(p + kXAhead, xld);
+        if constexpr (kDma) {
+            dma_slice(p + 2, (p + 2) % 3);   // the buffer of slice p-1, freed by the last barrier
+            stamp(p, 1);
+        } else {
+            store_slice((p + 1) & 1, xst);
+            stamp(p, 1);
+            load_slice(p + kXAhead, xld);
+        }
         load_entries(p + 3, wl, vl);
         stamp(p, 2);
         if (tracing) {
@@ -294,9 +385,10 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 #pragma unroll
             for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
         } else {
-            apply_band(xs[p & 1], wa, va);
+            apply_band(xs[kDma ? p % 3 : p & 1], wa, va);
         }
         stamp(p, 4);
+        if constexpr (kDma) wait_vmcnt<4 * CAP + kXv>();   // slice p+1 landed (entries may fly)
         if (!(ABL & 16)) __syncthreads();
         stamp(p, 5);
     };
@@ -304,7 +396,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // would share the loop latch and make hipcc's vmcnt bookkeeping merge the
     // break paths into the loop header (tight waits in the first step).  Steps
     // past the tile's last band see only dummy entries and apply nothing.
-    const int32_t nb4 = (nb + 3) & ~3;
+    const int32_t nb4 = (ABL & 256) ? 0 : (nb + 3) & ~3;
     for (int32_t p = 0; p < nb4; p += 4) {
         if constexpr (XR == 4) {
             step(p, X1, X0, W0, V0, W3, V3);
@@ -319,14 +411,20 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         }
     }
     if (tracing) return;
-    if (n_slabs == 1) {
-        for (int32_t i = tid; i < nr; i += THREADS) y[r0 + i] = yacc[i];
+    if (n_slabs == 1 || (ABL & 512)) {
+        const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int32_t i = 4 * (tid + q * THREADS);
+            if (i < nv) *reinterpret_cast<float4 *>(y + r0 + i) = *reinterpret_cast<const float4 *>(&yacc[i]);
+        }
+        for (int32_t i = nv + tid; i < nr; i += THREADS) y[r0 + i] = yacc[i];
     } else {
         // Publish this slab's sums (write-through, float4 where the rows allow),
         // then take a ticket.  Partials sit at a 4-aligned stride (ps).
         const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
         float *outp = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * ps + r0;
-        const bool vec = ((uintptr_t)(y + r0) & 15) == 0;   // partials are always aligned
+        const bool vec = y_vec;   // partials are always aligned
         const int32_t nr4 = vec ? (nr & ~3) : 0;
         const bool vec_out = slab != 0 || vec;
         const int32_t no4 = vec_out ? (nr & ~3) : 0;
@@ -352,7 +450,6 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             // Last tile of the block: every other slab has published.  y (slab 0)
             // plus the partials in slab order, every read an sc1 load; each thread
             // keeps its rows' loads of up to 4 slabs in flight at once.
-            constexpr int kQ = BROWS / (4 * THREADS);   // float4 rows per thread
             const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
             float4 acc[kQ];
 #pragma unroll
@@ -412,14 +509,25 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 template <int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
 hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                         float *y, float alpha, float beta, hipStream_t s) {
-    // x ring depth: 4 slices when a slice is 2 float4 per thread (blocked), 2 when
-    // it is 4 (exact: a deeper ring would not fit 128 VGPRs).
-    constexpr int XR = (1 << BAND_LOG2) / (4 * kXbThreads) <= 2 ? 4 : 2;
-    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),
-                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s,
-                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,
-                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets,
-                       alpha, beta);
+    // x staging: blocked (2 float4 per thread per slice) by LDS-DMA into three LDS
+    // buffers (2.5 % faster than its 4-slice register ring, which SM_XBAND_DMA=0
+    // selects for comparison); exact (4 float4 per slice, no room for a third
+    // 64 KiB buffer) through a 2-slice register ring.
+    constexpr int XRr = (1 << BAND_LOG2) / (4 * kXbThreads) <= 2 ? 4 : 2;
+    const char *dma_env = getenv("SM_XBAND_DMA");
+    const bool dma = XRr == 4 && !(dma_env && atoi(dma_env) == 0);
+#define SM_XBL(XR)                                                                              \
+    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),       \
+                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s, \
+                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
+                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
+                       alpha, beta)
+    if (dma) {
+        if constexpr (XRr == 4) SM_XBL(0);
+    } else {
+        SM_XBL(XRr);
+    }
+#undef SM_XBL
     return hipGetLastError();
 }
 
@@ -439,6 +547,13 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
         case 5: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 16: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 32: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 32>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 133: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 133>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 21: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 21>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 149: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 149>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 7: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 7>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 256: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 256>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 512: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 512>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 768: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 37: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         default: return hipErrorInvalidValue;
         }

@@ -133,25 +133,55 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
     out.word.assign((size_t)(total * 64), 0u);   // dummies (stored XOR dummy_word)
     out.val.assign((size_t)(total * 64), 0.0f);
 
+    // Lanes inside a chunk.  Order matters only within a row's segment (the
+    // kernel passes running sums from lane to lane and the last lane writes), so
+    // segments of 2+ terms take consecutive lanes first, then each single term of
+    // row r goes to lane (r mod 32) or 32 + (r mod 32) when free: the 32 lanes of
+    // each half then hit 32 distinct LDS banks when reading and writing their
+    // accumulators (dummy lanes write a per-lane scratch slot, bank = lane mod 32).
+    struct Seg { int32_t rl, s, e; };
+    auto emit_chunk = [&](int64_t p, int64_t c, const std::vector<Seg> &segs) {
+        bool used[64] = {false};
+        int next = 0;
+        auto put = [&](const Seg &g, int32_t k, int lane) {
+            const int64_t slot = c * 64 + lane;
+            const uint32_t cb = (uint32_t)(col[g.s + k] - p * band_cols);
+            out.word[(size_t)slot] = (cb | ((uint32_t)k << bits.col) |
+                                      ((uint32_t)g.rl << (bits.col + bits.rank))) ^
+                                     bits.dummy_word();
+            out.val[(size_t)slot] = val[g.s + k];
+            used[lane] = true;
+        };
+        for (const Seg &g : segs)
+            if (g.e - g.s > 1)
+                for (int32_t k = 0; k < g.e - g.s; k++) put(g, k, next++);
+        for (const Seg &g : segs) {
+            if (g.e - g.s != 1) continue;
+            const int bank = g.rl & 31;
+            int lane = !used[bank] ? bank : !used[32 + bank] ? 32 + bank : -1;
+            if (lane < 0)
+                for (lane = 63; used[lane]; lane--) {}
+            put(g, 0, lane);
+        }
+    };
     for_blocks([&](int64_t b) {
-        std::vector<int64_t> chunk((size_t)nb), fill((size_t)nb, 0);
+        std::vector<int64_t> chunk((size_t)nb);
+        std::vector<int32_t> fill((size_t)nb, 0);
+        std::vector<std::vector<Seg>> open((size_t)nb);
         for (int64_t p = 0; p < nb; p++) chunk[p] = out.chunk_start[(size_t)(b * nb + p)] - 1;
         walk(b, [&](int64_t p, int32_t rl, int32_t s, int32_t e) {
             const int32_t len = e - s;
             if (chunk[p] < out.chunk_start[(size_t)(b * nb + p)] || fill[p] + len > 64) {
+                if (!open[p].empty()) emit_chunk(p, chunk[p], open[p]);
+                open[p].clear();
                 chunk[p]++;
                 fill[p] = 0;
             }
-            for (int32_t k = 0; k < len; k++) {
-                const int64_t slot = chunk[p] * 64 + fill[p] + k;
-                const uint32_t cb = (uint32_t)(col[s + k] - p * band_cols);
-                out.word[(size_t)slot] = (cb | ((uint32_t)k << bits.col) |
-                                          ((uint32_t)rl << (bits.col + bits.rank))) ^
-                                         bits.dummy_word();
-                out.val[(size_t)slot] = val[s + k];
-            }
+            open[p].push_back(Seg{rl, s, e});
             fill[p] += len;
         });
+        for (int64_t p = 0; p < nb; p++)
+            if (!open[p].empty()) emit_chunk(p, chunk[p], open[p]);
     });
     return true;
 }
