@@ -77,7 +77,7 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
 // the x slice loads, bit 4 the entry loads, bit 16 the per-band barrier; the staged
 // slices are kept live so nothing upstream is dead-code removed; bit 128 skips the
 // slice stores into LDS (the loaded values kept live), 256 the whole band loop, 512
-// the slab hand-off and combine (plain stores instead).  Bit 32 records
+// the slab hand-off and combine (plain stores instead), 2048 everything (launch cost).  Bit 32 records
 // s_memtime stamps (tile 0, 6 per band per wave, bands < 32) into y[0, 3072).
 // Timing only: results are wrong.
 // XR: x slices held in registers (2 or 4): slice p+XR+(XR==2) is loaded at band p and
@@ -108,6 +108,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     constexpr int kScratch = kDma ? 0 : 64;     // per-lane write slots (no room with 3 buffers)
     __shared__ __attribute__((aligned(16))) float xs[kXBufs][BAND];
     __shared__ float yacc[BROWS + kScratch];   // + one scratch slot per lane (writes that land nowhere)
+    if (ABL & 2048) return;   // launch cost only
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -554,6 +555,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
         case 256: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 256>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 512: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 512>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 768: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 2048: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 2048>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 37: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         default: return hipErrorInvalidValue;
         }
