@@ -123,7 +123,8 @@ int32_t tile_nnz_setting() {
 // SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
 XbKind xband_kind_setting() {
     const char *e = getenv("SM_XBAND_KIND");
-    return (e && strcmp(e, "exact") == 0) ? kXbExact : kXbBlocked;
+    if (e && strcmp(e, "exact") == 0) return kXbExact;
+    return kXbBlocked;
 }
 
 bool want_xband(const sm_matrix *m) {
@@ -131,7 +132,8 @@ bool want_xband(const sm_matrix *m) {
     if (e && atoi(e) == 0) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
     if (e && atoi(e) == 1) return true;
-    const int rows_log2 = xband_kind_setting() == kXbExact ? kXbExactRowsLog2 : kXbBlockedRowsLog2;
+    const XbKind kind = xband_kind_setting();
+    const int rows_log2 = kind == kXbExact ? kXbExactRowsLog2 : kXbBlockedRowsLog2;
     const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
     const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
     const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
@@ -148,7 +150,7 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     XbandDev &d = m->plan.xb;
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
     int32_t n_slabs = 1;
-    if (kind == kXbBlocked) {
+    if (kind != kXbExact) {
         const int64_t want = (kXbTargetTiles + xh.n_blocks - 1) / xh.n_blocks;
         n_slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(want, xh.n_bands));
     }

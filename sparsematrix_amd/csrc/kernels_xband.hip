@@ -104,8 +104,15 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     static_assert(XR == 0 || XR == 2 || XR == 4, "x ring of 2 or 4 slices, or LDS-DMA");
     constexpr bool kDma = XR == 0;
     constexpr int kXAhead = XR == 4 ? 4 : 3;    // register ring: slice loaded at band p: p + kXAhead
-    constexpr int kXBufs = kDma ? 3 : 2;        // LDS x buffers
-    constexpr int kScratch = kDma ? 0 : 64;     // per-lane write slots (no room with 3 buffers)
+    // LDS: x buffers (three for LDS-DMA when they fit: two bands of lookahead),
+    // then per-lane scratch write slots when they fit too.
+    constexpr int kLds = 163840;
+    constexpr int kXBufs = kDma && 3 * BAND * 4 + BROWS * 4 <= kLds ? 3 : 2;
+    constexpr int kScratch = kXBufs * BAND * 4 + (BROWS + 64) * 4 <= kLds ? 64 : 0;
+    constexpr int kDmaAhead = kXBufs - 1;       // LDS-DMA: slice p + kDmaAhead issued at band p
+    // vmcnt at the end of band p that retires slice p+1 (issued kDmaAhead-1 bands
+    // earlier, each band issuing its slice then its entries: 2*CAP loads).
+    constexpr int kDmaWait = kDmaAhead == 2 ? 4 * CAP + kXv : 2 * CAP;
     __shared__ __attribute__((aligned(16))) float xs[kXBufs][BAND];
     __shared__ float yacc[BROWS + kScratch];   // + one scratch slot per lane (writes that land nowhere)
     if (ABL & 2048) return;   // launch cost only
@@ -320,13 +327,19 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         for (int q = 0; q < kQ; ++q)
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (kDma) {      // pending after: E1 D1 E2 (D0, E0 retired)
+    if constexpr (kDma && kDmaAhead == 2) {   // pending after: E1 D1 E2 (D0, E0 retired)
         load_entries(0, W0, V0);
         dma_slice(0, 0);
         load_entries(1, W1, V1);
         dma_slice(1, 1);
         load_entries(2, W2, V2);
-        wait_vmcnt<4 * CAP + kXv>();   // slice 0 landed
+        wait_vmcnt<kDmaWait>();   // slice 0 landed
+    } else if constexpr (kDma) {              // pending after: E2 (E0 E1 D0 retired)
+        load_entries(0, W0, V0);
+        load_entries(1, W1, V1);
+        dma_slice(0, 0);
+        load_entries(2, W2, V2);
+        wait_vmcnt<kDmaWait>();   // slice 0 landed
     } else if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
         load_slice(0, X0);
         load_slice(1, X1);
@@ -365,7 +378,8 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         stamp(p, 0);
         if (p + 3 >= cw + 64) advance_cs_window();   // this step reads cs[p+3], cs[p+4]
         if constexpr (kDma) {
-            dma_slice(p + 2, (p + 2) % 3);   // the buffer of slice p-1, freed by the last barrier
+            // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
+            dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
             stamp(p, 1);
         } else {
             store_slice((p + 1) & 1, xst);
@@ -386,10 +400,10 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 #pragma unroll
             for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
         } else {
-            apply_band(xs[kDma ? p % 3 : p & 1], wa, va);
+            apply_band(xs[kDma ? p % kXBufs : p & 1], wa, va);
         }
         stamp(p, 4);
-        if constexpr (kDma) wait_vmcnt<4 * CAP + kXv>();   // slice p+1 landed (entries may fly)
+        if constexpr (kDma) wait_vmcnt<kDmaWait>();   // slice p+1 landed (entries may fly)
         if (!(ABL & 16)) __syncthreads();
         stamp(p, 5);
     };
@@ -460,10 +474,11 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
                 acc[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
                                      __uint_as_float(u.z), __uint_as_float(u.w));
             }
-            for (int32_t s0 = 1; s0 < n_slabs; s0 += 4) {
-                u32x4 pv[4][kQ];
+            constexpr int kG = kQ >= 8 ? 2 : 4;   // slabs in flight at once (VGPR budget)
+            for (int32_t s0 = 1; s0 < n_slabs; s0 += kG) {
+                u32x4 pv[kG][kQ];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kG; ++j) {
                     const int32_t sl = min(s0 + j, n_slabs - 1);
                     const __amdgpu_buffer_rsrc_t p_src =
                         rsrc(partials + (int64_t)(sl - 1) * ps + r0, (uint64_t)nr * 4);
@@ -473,7 +488,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
                             p_src, 16u * (uint32_t)(tid + q * THREADS), 0, kAuxSc1);
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kG; ++j) {
                     if (s0 + j >= n_slabs) break;
 #pragma unroll
                     for (int q = 0; q < kQ; ++q) {
