@@ -144,14 +144,16 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     const XbKind kind = xband_kind_setting();
     const XbBits bits = kind == kXbExact ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
                                          : xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
+    const int threads = kXbThreads;
+    const int64_t target_tiles = (int64_t)kXbTargetTiles * (kXbThreads / threads);   // fill the CUs
     XbandHost xh;
-    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, xh))
+    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, threads / 64, xh))
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     XbandDev &d = m->plan.xb;
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
     int32_t n_slabs = 1;
     if (kind != kXbExact) {
-        const int64_t want = (kXbTargetTiles + xh.n_blocks - 1) / xh.n_blocks;
+        const int64_t want = (target_tiles + xh.n_blocks - 1) / xh.n_blocks;
         n_slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(want, xh.n_bands));
     }
     // Slabs of whole groups of 4 bands (the kernel steps bands 4 at a time).
@@ -175,6 +177,7 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
         SM_TRY_HIP(hipMemcpy(d.d_val, xh.val.data(), xh.val.size() * 4, hipMemcpyHostToDevice));
     }
     d.kind = kind;
+    d.threads = threads;
     d.block_rows = xh.block_rows;
     d.band_cols = xh.band_cols;
     d.n_bands = xh.n_bands;

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     constexpr int kXAhead = XR == 4 ? 4 : 3;    // register ring: slice loaded at band p: p + kXAhead
     // LDS: x buffers (three for LDS-DMA when they fit: two bands of lookahead),
     // then per-lane scratch write slots when they fit too.
-    constexpr int kLds = 163840;
+    constexpr int kLds = 163840 / (1024 / THREADS);   // LDS per CU / workgroups per CU
     constexpr int kXBufs = kDma && 3 * BAND * 4 + BROWS * 4 <= kLds ? 3 : 2;
     constexpr int kScratch = kXBufs * BAND * 4 + (BROWS + 64) * 4 <= kLds ? 64 : 0;
     constexpr int kDmaAhead = kXBufs - 1;       // LDS-DMA: slice p + kDmaAhead issued at band p
@@ -522,19 +522,19 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     if (ABL && beta == -12345.0f) y[tid] = xs[0][tid] + xs[1][tid];   // keep the staging live
 }
 
-template <int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
 hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                         float *y, float alpha, float beta, hipStream_t s) {
     // x staging: blocked (2 float4 per thread per slice) by LDS-DMA into three LDS
     // buffers (2.5 % faster than its 4-slice register ring, which SM_XBAND_DMA=0
     // selects for comparison); exact (4 float4 per slice, no room for a third
     // 64 KiB buffer) through a 2-slice register ring.
-    constexpr int XRr = (1 << BAND_LOG2) / (4 * kXbThreads) <= 2 ? 4 : 2;
+    constexpr int XRr = (1 << BAND_LOG2) / (4 * THREADS) <= 2 ? 4 : 2;
     const char *dma_env = getenv("SM_XBAND_DMA");
     const bool dma = XRr == 4 && !(dma_env && atoi(dma_env) == 0);
 #define SM_XBL(XR)                                                                              \
-    hipLaunchKernelGGL((spmv_xband_kernel<kXbThreads, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),       \
-                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(kXbThreads), 0, s, \
+    hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),          \
+                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
                        xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
                        alpha, beta)
@@ -547,38 +547,38 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
     return hipGetLastError();
 }
 
-template <int BAND_LOG2, int ROWS_LOG2>
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2>
 hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                        float *y, float alpha, float beta, hipStream_t s) {
-    const int waves = kXbThreads / 64;
+    const int waves = THREADS / 64;
     const int64_t cap = (xb.max_chunks_per_band + waves - 1) / waves;
     const char *abl_env = getenv("SM_XBAND_ABLATE");   // development only
     const int abl = abl_env ? atoi(abl_env) : 0;
     if (abl) {
         if (cap > kXbMaxCap) return hipErrorInvalidValue;
         switch (abl) {
-        case 1: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 2: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 4: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 5: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 16: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 32: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 32>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 133: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 133>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 21: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 21>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 149: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 149>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 7: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 7>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 256: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 256>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 512: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 512>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 768: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 2048: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 2048>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 37: return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 1: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 2: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 4: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 5: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 16: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 32: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 32>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 133: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 133>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 21: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 21>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 149: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 149>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 7: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 7>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 256: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 256>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 512: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 512>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 768: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 2048: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 2048>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 37: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         default: return hipErrorInvalidValue;
         }
     }
-    if (cap <= 1) return launch_tiles<BAND_LOG2, ROWS_LOG2, 1, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= 2) return launch_tiles<BAND_LOG2, ROWS_LOG2, 2, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= 3) return launch_tiles<BAND_LOG2, ROWS_LOG2, 3, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= kXbMaxCap) return launch_tiles<BAND_LOG2, ROWS_LOG2, 4, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 1) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 1, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 2) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 2, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 3) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 3, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= kXbMaxCap) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     return hipErrorInvalidValue;
 }
 
@@ -595,10 +595,10 @@ hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     hipError_t e = hipErrorInvalidValue;
     if (xb.kind == kXbExact && xb.band_cols == 1 << kXbExactBandLog2 &&
         xb.block_rows <= 1 << kXbExactRowsLog2)
-        e = launch_kind<kXbExactBandLog2, kXbExactRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        e = launch_kind<kXbThreads, kXbExactBandLog2, kXbExactRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     else if (xb.kind == kXbBlocked && xb.band_cols == 1 << kXbBlockedBandLog2 &&
              xb.block_rows <= 1 << kXbBlockedRowsLog2)
-        e = launch_kind<kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        e = launch_kind<kXbThreads, kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     return e;
 }
 

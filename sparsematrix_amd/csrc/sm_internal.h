@@ -36,6 +36,7 @@ struct alignas(16) Chunk {
 // Device copy of the column-band layout (xband.h).
 struct XbandDev {
     int32_t kind = 0;                 // XbKind; 0 when not built
+    int32_t threads = 0;              // workgroup size of the kind
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int32_t n_slabs = 1, slab_bands = 0;   // tiles = n_blocks * n_slabs
     int64_t n_chunks = 0;

@@ -34,17 +34,17 @@ namespace smamd {
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
                               int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
-                              XbandHost &out);
+                              int waves, XbandHost &out);
 
 // Largest block height (<= 2^bits.row, >= 64) whose bands fit the kernel's
 // register capacity (kXbMaxCap chunks per wave per band).
 bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, XbBits bits, XbandHost &out) {
+                 int64_t n_cols, XbBits bits, int waves, XbandHost &out) {
     if (bits.col < 8 || bits.row < 6 || bits.rank < 2 || bits.col + bits.rank + bits.row != 32)
         return false;
     for (int32_t br = 1 << bits.row; br >= 64; br /= 2) {
         out.too_dense = false;
-        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, bits, out)) return true;
+        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, bits, waves, out)) return true;
         if (!out.too_dense) return false;   // not a capacity problem: halving will not help
     }
     return false;
@@ -52,7 +52,7 @@ bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
                               int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
-                              XbandHost &out) {
+                              int waves, XbandHost &out) {
     out = XbandHost();
     if (n_rows <= 0 || n_cols <= 0) return false;
     const int32_t band_cols = 1 << bits.col;
@@ -126,7 +126,7 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
     for (int64_t i = 0; i < nblk * nb; i++)
         out.max_chunks_per_band = std::max<int64_t>(out.max_chunks_per_band, chunks_of[i]);
     // The kernel holds a band's chunks in registers: at most kXbMaxCap per wave.
-    if (out.max_chunks_per_band > (int64_t)kXbMaxCap * (kXbThreads / 64)) {
+    if (out.max_chunks_per_band > (int64_t)kXbMaxCap * waves) {
         out.too_dense = true;
         return false;
     }

@@ -49,6 +49,6 @@ struct XbandHost {
 // for 64-row blocks, or size limits).  The block height starts at 2^bits.row and
 // halves while a band overflows the kernel's register capacity.
 bool xband_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, XbBits bits, XbandHost &out);
+                 int64_t n_cols, XbBits bits, int waves, XbandHost &out);
 
 }  // namespace smamd

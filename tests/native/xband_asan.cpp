@@ -14,8 +14,8 @@
 
 using namespace smamd;
 
-static int check(XbBits bits, int64_t n_rows, int64_t n_cols, int per_row, unsigned seed,
-                 bool expect_ok) {
+static int check(XbBits bits, int waves, int64_t n_rows, int64_t n_cols, int per_row,
+                 unsigned seed, bool expect_ok) {
     std::mt19937 rng(seed);
     std::vector<int32_t> rp(n_rows + 1), col;
     std::vector<float> val;
@@ -28,12 +28,12 @@ static int check(XbBits bits, int64_t n_rows, int64_t n_cols, int per_row, unsig
         rp[r + 1] = (int32_t)col.size();
     }
     XbandHost xh;
-    const bool ok = xband_build(rp.data(), col.data(), val.data(), n_rows, n_cols, bits, xh);
+    const bool ok = xband_build(rp.data(), col.data(), val.data(), n_rows, n_cols, bits, waves, xh);
     if (ok != expect_ok) { printf("FAIL build=%d expected %d\n", ok, expect_ok); return 1; }
     if (!ok) return 0;
     if (xh.block_rows > (1 << bits.row) || xh.band_cols != (1 << bits.col)) {
         printf("FAIL geometry\n"); return 1; }
-    if (xh.max_chunks_per_band > kXbMaxCap * (kXbThreads / 64)) {
+    if (xh.max_chunks_per_band > kXbMaxCap * waves) {
         printf("FAIL register capacity\n"); return 1; }
     const uint32_t colmask = (1u << bits.col) - 1u, rankmask = (1u << bits.rank) - 1u;
     std::vector<std::vector<std::pair<int32_t, float>>> got(n_rows);
@@ -81,14 +81,16 @@ int main() {
     const XbBits exact = xb_bits(kXbExactBandLog2, kXbExactRowsLog2);
     const XbBits blocked = xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
     int bad = 0;
-    for (XbBits bits : {exact, blocked}) {
-        bad += check(bits, 200003, 300001, 16, 1, true);
-        bad += check(bits, 9000, 70001, 40, 2, true);    // dense bands: smaller blocks
-        bad += check(bits, 4096, 32768, 7, 3, true);
-        bad += check(bits, 5000, 1000, 5, 4, true);
-        bad += check(bits, 5000, 40000, 8, 5, true);
-        bad += check(bits, 70000, 1000003, 16, 7, true);
-        bad += check(bits, 300, 20000, 400, 6, false);   // a row's segment too long for the rank field
+    const struct { XbBits bits; int waves; } kinds[] = {
+        {exact, kXbThreads / 64}, {blocked, kXbThreads / 64}};
+    for (const auto &k : kinds) {
+        bad += check(k.bits, k.waves, 200003, 300001, 16, 1, true);
+        bad += check(k.bits, k.waves, 9000, 70001, 40, 2, true);    // dense bands: smaller blocks
+        bad += check(k.bits, k.waves, 4096, 32768, 7, 3, true);
+        bad += check(k.bits, k.waves, 5000, 1000, 5, 4, true);
+        bad += check(k.bits, k.waves, 5000, 40000, 8, 5, true);
+        bad += check(k.bits, k.waves, 70000, 1000003, 16, 7, true);
+        bad += check(k.bits, k.waves, 300, 20000, 400, 6, false);   // a row's segment too long for the rank field
     }
     printf(bad ? "xband_asan: FAILED\n" : "xband_asan: ok\n");
     return bad ? 1 : 0;

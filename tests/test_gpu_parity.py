@@ -418,14 +418,16 @@ def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
 @pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 300001, 16), (9000, 70001, 40),
                                                    (70000, 1000003, 16), (5000, 1000, 5),
                                                    (40000, 20000, 3)])
-def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row):
+@pytest.mark.parametrize("kind,code", [("blocked", 2)])
+def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row, kind, code):
     """Blocked band layout (16K-row blocks, column slabs): within the Σ|terms| bound
     of the reference order; bit-identical when the matrix is a single slab; the
     AUTO path runs it; beta = 0 drops NaN only where the reference does."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols + 7)
-    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
+        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
     info = M.info()
-    assert info["has_xband"] == 2, info
+    assert info["has_xband"] == code, info
     assert info["xband_block_rows"] >= 64 and info["xband_slabs"] >= 1
     rng = np.random.default_rng(5)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
