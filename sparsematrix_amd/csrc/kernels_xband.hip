@@ -138,23 +138,24 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // cs[cw + 64 + l] (hi), tile-relative; read by readlane with a branch-free
     // select.  Every 64 bands the window advances: hi (loaded 64 bands earlier)
     // becomes lo and the next hi is prefetched -- no load is waited for at once.
+    // The raw table values are kept (c_first is subtracted after the readlane), so
+    // the prefetched hi half is not touched -- and not waited for -- until it
+    // becomes lo 64 bands later.
     int32_t cw = 0;
-    int32_t cs_lo = csg[min(lane, nb)] - c_first;
-    int32_t cs_hi = csg[min(64 + lane, nb)] - c_first;
+    int32_t cs_lo = csg[min(lane, nb)];
+    int32_t cs_hi = csg[min(64 + lane, nb)];
     auto advance_cs_window = [&]() {
         cw += 64;
         cs_lo = cs_hi;
-        cs_hi = csg[min(cw + 64 + lane, nb)] - c_first;
+        cs_hi = csg[min(cw + 64 + lane, nb)];
     };
     auto cs_at = [&](int32_t i) -> int32_t {   // i in [cw, cw + 128), wave-uniform
         const int32_t j = i - cw;
         const int32_t lo = __builtin_amdgcn_readlane(cs_lo, j & 63);
         const int32_t hi = __builtin_amdgcn_readlane(cs_hi, j & 63);
-        return j < 64 ? lo : hi;
+        return (j < 64 ? lo : hi) - c_first;
     };
 
-    // Slices past the tile's last band (the pipeline's run-out) load from past the
-    // descriptor's range: no memory request (they would be 4 bands of wasted x).
     auto load_slice = [&](int32_t p, float4 *xr) {
 #pragma unroll
         for (int k = 0; k < kXv; ++k) {
