@@ -15,7 +15,7 @@ OBJS      = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
             $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS      = include/sparsematrix.h $(wildcard $(CSRC)/*.h)
 
-all: $(LIB) $(SHIM) oracle compat
+all: $(LIB) $(SHIM) oracle compat build/blas_test
 
 # C++ drop-in shim (reference class/kernel signatures) over the C ABI
 $(SHIM): $(CSRC)/sblas_shim.cpp include/sblas/sparse-matrix.h include/sblas/kernel.h $(LIB)
@@ -36,6 +36,12 @@ build/compat/%: $(REFSRC)/%.cc $(SHIM)
 else
 compat:
 endif
+
+# The reference harness's command line over the GPU backend (tools/blas_test.cc).
+build/blas_test: tools/blas_test.cc include/sblas/sparse-matrix.h $(SHIM)
+	@mkdir -p build
+	$(HIPCC) -O2 -std=c++17 -Iinclude/sblas -o $@ $< -L$(PKG) -lsblas -lsparsematrix_amd \
+	    -Wl,-rpath,'$$ORIGIN/../$(PKG)'
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -6,10 +6,14 @@ for every fast-kernel row of <= SM_SERIAL_ROW_MAX terms; |err| <= 1e-6 sum|terms
 for longer rows.  Full BASELINE sizes are checked through size-independent
 properties (stream == parity bit-for-bit on 16-term rows, linearity).
 """
+import os
+
 import numpy as np
 import pytest
 
 import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 from golden_util import bits_equal, case_names, load_case
 from gpu_util import (assert_terms_close, bits, skewed_csr, to_dev, to_host, torch_dev,
                       uniform_csr)
@@ -445,6 +449,39 @@ def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row, kind, code):
             assert_terms_close(got, want, absum)
 
 
+@pytest.mark.parametrize("kind", ["exact", "blocked"])
+def test_xband_special_values(sm, kind):
+    """Inf/NaN in x and in the stored values propagate exactly as in the reference; the
+    dummy lanes (column 0, value 0) that see x[0] = inf compute NaN but never land."""
+    n_rows, n_cols = 30000, 50000
+    rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77)
+    va = va.copy()
+    va[::997] = np.inf
+    va[5::1009] = np.nan
+    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
+        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    assert M.info()["has_xband"] in (1, 2)
+    rng = np.random.default_rng(8)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    x[0] = np.inf                      # what every dummy lane reads
+    x[1::4999] = -np.inf
+    x[2::7001] = np.nan
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    for alpha, beta in ((1.0, 1.0), (0.5, 0.0)):
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, alpha, beta, algo="xband")
+        got = to_host(y)
+        if M.info()["xband_slabs"] == 1:
+            assert np.array_equal(bits(got), bits(want))
+        else:
+            assert np.array_equal(np.isnan(got), np.isnan(want))
+            fin = np.isfinite(want)
+            assert np.array_equal(got[~fin & ~np.isnan(want)], want[~fin & ~np.isnan(want)])
+            assert_terms_close(got[fin], want[fin], absum[fin])
+
+
 def test_xband_not_applicable_falls_back(sm):
     """A row with more terms inside one band than the rank field holds cannot use the
     layout: the matrix is still served (stream kernel) and results stay correct;
@@ -478,3 +515,28 @@ def test_xband_not_applicable_falls_back(sm):
     # the Python mirror refuses operands too small for the matrix (the C ABI cannot see sizes)
     with pytest.raises(ValueError):
         M2.spmv(xb[1:], to_dev(y0), algo="xband")
+
+
+@pytest.mark.gpu
+def test_blas_test_cli():
+    """tools/blas_test: the reference harness's command line (m:n:k doubling sweeps, check
+    flag, ';'-separated filter with '-' exclusion, markdown timing table) over the GPU
+    backend, every result within the reference's own tolerance."""
+    import subprocess
+    exe = os.path.join(ROOT, "build", "blas_test")
+    if not os.path.exists(exe):
+        pytest.skip("build/blas_test not built")
+    r = subprocess.run([exe, "4:16", "64", "128:512", "1"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("|")]
+    assert lines[0].startswith("| | 4x64x128 |") and lines[0].count("|") == 1 + 9 + 1, lines[0]
+    names = {l.split("|")[1].strip() for l in lines[1:]}
+    assert names == {"cpu_sgemm_baseline", "sgemm_sparse", "sgemm_sparse_device"}, names
+    assert "failed" not in r.stdout
+    # first matching pattern decides (blas_test.h:20-26): exclude the device variant first
+    r = subprocess.run([exe, "8", "128", "256", "1", "-device;sparse"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    names = {l.split("|")[1].strip() for l in r.stdout.splitlines()[1:] if l.startswith("|")}
+    assert names == {"sgemm_sparse"}, r.stdout
