@@ -24,7 +24,8 @@ def main(root):
     for k, ctrs in acc.items():
         if "smamd" not in k:
             continue
-        short = k.split("(")[0].replace("void smamd::(anonymous namespace)::", "")
+        short = k.replace("void ", "").replace("smamd::(anonymous namespace)::", "")
+        short = short.split("(")[0][:90]
         print(short)
         for c in sorted(ctrs):
             v = ctrs[c]
