@@ -156,9 +156,9 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
         const int64_t want = (target_tiles + xh.n_blocks - 1) / xh.n_blocks;
         n_slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(want, xh.n_bands));
     }
-    // Slabs of whole groups of 4 bands (the kernel steps bands 4 at a time).
+    // Slabs of whole groups of 8 bands (the kernel steps bands 4 or 8 at a time).
     int32_t slab_bands = (xh.n_bands + n_slabs - 1) / n_slabs;
-    slab_bands = (slab_bands + 3) & ~3;
+    slab_bands = (slab_bands + 7) & ~7;
     n_slabs = (xh.n_bands + slab_bands - 1) / slab_bands;
     std::vector<int32_t> cs32(xh.chunk_start.size());
     for (size_t i = 0; i < cs32.size(); i++) cs32[i] = (int32_t)xh.chunk_start[i];

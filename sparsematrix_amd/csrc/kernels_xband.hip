@@ -278,13 +278,17 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         }
     };
 
-    // Register rings with static roles (the band loop is unrolled by 4, so no
-    // register ever moves -- a move would make hipcc wait for the load that
-    // filled it): x slice q lives in X[q % XR], the entries of band q in
-    // W/V[q % 4].
-    float4 X0[kXv], X1[kXv], X2[XR == 4 ? kXv : 1], X3[XR == 4 ? kXv : 1];
-    uint32_t W0[CAP], W1[CAP], W2[CAP], W3[CAP];
-    float V0[CAP], V1[CAP], V2[CAP], V3[CAP];
+    // Register rings with static roles (the band loop is unrolled by kER, so every
+    // ring index is a compile-time constant and no register ever moves -- a move
+    // would make hipcc wait for the load that filled it): x slice q lives in
+    // X[q % XR], the entries of band q in W/V[q % kER], loaded kEAhead bands early.
+    constexpr int kEAhead = 3;                  // entries' lookahead (5 measured: no gain)
+    constexpr int kER = kEAhead > 3 ? 8 : 4;    // entry ring = loop unroll
+    constexpr int kXR = XR > 0 ? XR : 1;
+    static_assert(kER % kXR == 0 && kEAhead < kER, "ring sizes");
+    float4 X[kXR][kXv];
+    uint32_t W[kER][CAP];
+    float V[kER][CAP];
     // Accumulators first: this loop's own loads are drained before the pipeline
     // starts.  Then the prologue issues its loads in exactly the order the loop
     // leaves them pending at its back edge, so hipcc's vmcnt bookkeeping merges
@@ -328,46 +332,50 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         for (int q = 0; q < kQ; ++q)
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if constexpr (kDma && kDmaAhead == 2) {   // pending after: E1 D1 E2 (D0, E0 retired)
-        load_entries(0, W0, V0);
+    // Prologue: the loads the loop expects in flight, issued in its order
+    // (per band q: slice q+kDmaAhead, then entries q+kEAhead).
+    if constexpr (kDma && kDmaAhead == 2) {   // pending after: E(A-2) D1 E(A-1)
+#pragma unroll
+        for (int q = 0; q <= kEAhead - 3; ++q) load_entries(q, W[q], V[q]);
         dma_slice(0, 0);
-        load_entries(1, W1, V1);
+        load_entries(kEAhead - 2, W[kEAhead - 2], V[kEAhead - 2]);
         dma_slice(1, 1);
-        load_entries(2, W2, V2);
+        load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
         wait_vmcnt<kDmaWait>();   // slice 0 landed
-    } else if constexpr (kDma) {              // pending after: E2 (E0 E1 D0 retired)
-        load_entries(0, W0, V0);
-        load_entries(1, W1, V1);
+    } else if constexpr (kDma) {              // pending after: E(A-1)
+#pragma unroll
+        for (int q = 0; q <= kEAhead - 2; ++q) load_entries(q, W[q], V[q]);
         dma_slice(0, 0);
-        load_entries(2, W2, V2);
+        load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
         wait_vmcnt<kDmaWait>();   // slice 0 landed
     } else if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
-        load_slice(0, X0);
-        load_slice(1, X1);
-        load_entries(0, W0, V0);
-        load_slice(2, X2);
-        load_entries(1, W1, V1);
-        load_slice(3, X3);
-        load_entries(2, W2, V2);
-        store_slice(0, X0);
+        load_slice(0, X[0]);
+        load_slice(1, X[1]);
+        load_entries(0, W[0], V[0]);
+        load_slice(2, X[2 % kXR]);
+        load_entries(1, W[1], V[1]);
+        load_slice(3, X[3 % kXR]);
+        load_entries(2, W[2], V[2]);
+        store_slice(0, X[0]);
     } else {                   // pending after: E0 X1 E1 X0 E2
-        load_slice(0, X0);
-        load_entries(0, W0, V0);
-        load_slice(1, X1);
-        load_entries(1, W1, V1);
-        store_slice(0, X0);
-        load_slice(2, X0);
-        load_entries(2, W2, V2);
+        load_slice(0, X[0]);
+        load_entries(0, W[0], V[0]);
+        load_slice(1, X[1 % kXR]);
+        load_entries(1, W[1], V[1]);
+        store_slice(0, X[0]);
+        load_slice(2, X[0]);
+        load_entries(2, W[2], V[2]);
     }
     __syncthreads();
 
-    // Band p: buffer p&1 holds slice p (visible); the ring holds slice p+1.  One
-    // barrier per band: the stores of slice p+1 into buffer (p+1)&1 (freed by the
-    // previous barrier) and this band's reads of buffer p&1 both finish before
-    // it.  Slice p+kXAhead goes to the ring slot freed last (XR == 4: slice p's,
-    // stored a band ago; XR == 2: slice p+1's, stored just now); entries of band
-    // p+3 reuse the set of band p-1.  Loads past the tile's last band read the
-    // next slab's data or zeros (range-checked descriptors) and are never applied.
+    // Band p (register staging): buffer p&1 holds slice p (visible); the ring holds
+    // slice p+1.  One barrier per band: the stores of slice p+1 into buffer (p+1)&1
+    // (freed by the previous barrier) and this band's reads of buffer p&1 both
+    // finish before it.  Slice p+kXAhead goes to the ring slot freed last (XR == 4:
+    // slice p's, stored a band ago; XR == 2: slice p+1's, stored just now).  LDS-DMA:
+    // slice p+kDmaAhead goes straight into the buffer freed by the last barrier.
+    // Entries of band p+kEAhead reuse the set of band p+kEAhead-kER.  Loads past the
+    // tile's last band are sent past the descriptors' ranges and never applied.
     const bool tracing = (ABL & 32) && blockIdx.x == 0;
     auto stamp = [&](int32_t p, int k) {
         if (!tracing || p >= 32) return;
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     auto step = [&](int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va, uint32_t *wl,
                     float *vl) {
         stamp(p, 0);
-        if (p + 3 >= cw + 64) advance_cs_window();   // this step reads cs[p+3], cs[p+4]
+        if (p + kEAhead >= cw + 64) advance_cs_window();   // reads cs[p+A], cs[p+A+1]
         if constexpr (kDma) {
             // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
             dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             stamp(p, 1);
             load_slice(p + kXAhead, xld);
         }
-        load_entries(p + 3, wl, vl);
+        load_entries(p + kEAhead, wl, vl);
         stamp(p, 2);
         if (tracing) {
 #pragma unroll
@@ -408,22 +416,19 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         if (!(ABL & 16)) __syncthreads();
         stamp(p, 5);
     };
-    // Whole groups of 4 bands, no early exit: a break out of the unrolled body
+    // Whole groups of kER bands, no early exit: a break out of the unrolled body
     // would share the loop latch and make hipcc's vmcnt bookkeeping merge the
     // break paths into the loop header (tight waits in the first step).  Steps
     // past the tile's last band see only dummy entries and apply nothing.
-    const int32_t nb4 = (ABL & 256) ? 0 : (nb + 3) & ~3;
-    for (int32_t p = 0; p < nb4; p += 4) {
-        if constexpr (XR == 4) {
-            step(p, X1, X0, W0, V0, W3, V3);
-            step(p + 1, X2, X1, W1, V1, W0, V0);
-            step(p + 2, X3, X2, W2, V2, W1, V1);
-            step(p + 3, X0, X3, W3, V3, W2, V2);
-        } else {
-            step(p, X1, X1, W0, V0, W3, V3);
-            step(p + 1, X0, X0, W1, V1, W0, V0);
-            step(p + 2, X1, X1, W2, V2, W1, V1);
-            step(p + 3, X0, X0, W3, V3, W2, V2);
+    const int32_t nbu = (ABL & 256) ? 0 : (nb + kER - 1) / kER * kER;
+    for (int32_t p = 0; p < nbu; p += kER) {
+#pragma unroll
+        for (int u = 0; u < kER; ++u) {
+            // x: store slice p+u+1 from X[(u+1) % XR]; load slice p+u+kXAhead into the
+            // slot freed last (XR 4: slice p+u's; XR 2: the one just stored).
+            float4 *xst = X[(u + 1) % kXR];
+            float4 *xld = X[(XR == 4 ? u : u + 1) % kXR];
+            step(p + u, xst, xld, W[u], V[u], W[(u + kEAhead) % kER], V[(u + kEAhead) % kER]);
         }
     }
     if (tracing) return;
