@@ -199,7 +199,7 @@ def main():
                 "gflops": round(2.0 * nnz * N / (sm_ms * 1e-3) / 1e9, 1),
                 "hbm_gbs": round(sb / (sm_ms * 1e-3) / 1e9, 1),
                 "hbm_frac": round(sb / (sm_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                "kernel": "spmm_rowpanel_kernel<8>", "mfma": "not used (fp32 SpMM at "
+                "kernel": "spmm_rowpanel2_kernel<8>", "mfma": "not used (fp32 SpMM at "
                 "~2 flop/B is HBM/gather bound; see DESIGN.md)"}
         del X, Y
 

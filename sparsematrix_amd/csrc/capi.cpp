@@ -632,8 +632,8 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
                         ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
     if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
-        e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, X, ldx, Y, ldy, alpha,
-                                 beta, s);
+        e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X,
+                                 ldx, m->n_cols, Y, ldy, alpha, beta, s);
     else if (algo >= SM_ALGO_AUTO && algo <= SM_ALGO_VECTOR)
         e = launch_spmm_generic(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, X, ldx, 1, Y, ldy, 1,
                                 alpha, beta, true, s);

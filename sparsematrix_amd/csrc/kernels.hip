@@ -35,6 +35,7 @@ __device__ __forceinline__ float term(float xv, float v, float alpha) {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Streamed (read-once) 16-byte loads of val/col.  SM_NT_LOADS selects the
 // non-temporal cache policy (measured both ways).
@@ -315,6 +316,81 @@ __global__ __launch_bounds__(256) void spmm_rowpanel_kernel(
     if (active) *reinterpret_cast<float4 *>(yp) = acc;
 }
 
+// Range-checked buffer descriptor: loads past `bytes` read 0 and make no memory
+// request, so a padded slot needs no branch (a branch around a load makes hipcc
+// drain vmcnt before the next one).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel_rsrc(const void *base, uint64_t bytes) {
+    const uint32_t nb = bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)nb,
+                                             0x00020000);
+}
+
+// SpMM row panel, gather-pipelined: like spmm_rowpanel_kernel (G lanes per output row,
+// lane g owns Y[r, 4g:4g+4]) but a row's terms go in groups of UU: the group's
+// (col, val) are loaded at once (UU/G per lane, broadcast by shuffles), then all UU
+// X-row gathers are in flight together -- branch-free range-checked buffer loads,
+// padded slots sent past the range -- and the terms are added in stored order
+// (padded slots skipped by a select, so the sum is bit-identical).  Requires X
+// (x_rows * ldx floats) under 4 GiB.
+template <int G>
+__global__ __launch_bounds__(256) void spmm_rowpanel2_kernel(
+    int32_t n, int32_t nrhs, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const float *__restrict__ val, int32_t nnz, const float *__restrict__ X, int64_t ldx,
+    int64_t x_rows, float *__restrict__ Y, int64_t ldy, float alpha, float beta) {
+    constexpr int UU = 16 > G ? 16 : G;   // terms per group
+    constexpr int T = UU / G;             // (col, val) loads per lane per group
+    constexpr uint32_t kOob = 0xFFFFFFF0u;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t r = (int32_t)(gid / G);
+    const int g = (int)(gid % G);
+    if (r >= n) return;   // whole groups of G lanes
+    const bool active = 4 * g < nrhs;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float *yp = Y + (int64_t)r * ldy + 4 * g;
+    if (active) acc = *reinterpret_cast<const float4 *>(yp);
+    if (beta != 1.0f) {
+        acc.x = mul_rn(acc.x, beta); acc.y = mul_rn(acc.y, beta);
+        acc.z = mul_rn(acc.z, beta); acc.w = mul_rn(acc.w, beta);
+    }
+    const __amdgpu_buffer_rsrc_t c_src = panel_rsrc(col, (uint64_t)nnz * 4);
+    const __amdgpu_buffer_rsrc_t v_src = panel_rsrc(val, (uint64_t)nnz * 4);
+    const __amdgpu_buffer_rsrc_t x_src = panel_rsrc(X, (uint64_t)x_rows * ldx * 4);
+    const int32_t a = rp[r];
+    const int32_t e = rp[r + 1];
+    for (int32_t b0 = a; b0 < e; b0 += UU) {
+        int32_t ci[T];
+        float vi[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int32_t i = b0 + g + G * t;
+            const uint32_t off = i < e ? 4u * (uint32_t)i : kOob;
+            ci[t] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(c_src, off, 0, 0);
+            vi[t] = mul_rn(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, 0)),
+                           alpha);
+        }
+        const int cnt = min(UU, e - b0);
+        u32x4 xv[UU];
+#pragma unroll
+        for (int j = 0; j < UU; ++j) {
+            const int32_t cj = __shfl(ci[j / G], j % G, G);
+            const uint32_t off = (j < cnt && active)
+                                     ? 4u * (uint32_t)((int64_t)cj * ldx + 4 * g)
+                                     : kOob;
+            xv[j] = __builtin_amdgcn_raw_buffer_load_b128(x_src, off, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < UU; ++j) {
+            const float vj = __shfl(vi[j / G], j % G, G);
+            const float4 s4 = make_float4(add_rn(acc.x, mul_rn(__uint_as_float(xv[j].x), vj)),
+                                          add_rn(acc.y, mul_rn(__uint_as_float(xv[j].y), vj)),
+                                          add_rn(acc.z, mul_rn(__uint_as_float(xv[j].z), vj)),
+                                          add_rn(acc.w, mul_rn(__uint_as_float(xv[j].w), vj)));
+            if (j < cnt) acc = s4;
+        }
+    }
+    if (active) *reinterpret_cast<float4 *>(yp) = acc;
+}
+
 template <bool RHS_FASTEST>
 __global__ __launch_bounds__(256) void spmm_generic_kernel(
     int32_t n, int32_t nrhs, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
@@ -470,16 +546,27 @@ hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const
 }
 
 hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
-                                const float *val, const float *X, int64_t ldx, float *Y,
-                                int64_t ldy, float alpha, float beta, hipStream_t s) {
+                                const float *val, int32_t nnz, const float *X, int64_t ldx,
+                                int64_t x_rows, float *Y, int64_t ldy, float alpha, float beta,
+                                hipStream_t s) {
     if (n <= 0) return hipSuccess;
     int G = 1;
     while (4 * G < nrhs) G <<= 1;
     const unsigned grid = blocks_for((int64_t)n * G);
+    // The gather-pipelined kernel while its X descriptor can span X (< 4 GiB) and a
+    // group's gathers fit the registers (G <= 16, i.e. N <= 64); SM_SPMM_OLD=1
+    // (development) keeps the one-group-at-a-time kernel for comparison.
+    const char *old_env = getenv("SM_SPMM_OLD");
+    const bool pipelined = !(old_env && atoi(old_env) != 0) && G <= 16 &&
+                           (uint64_t)x_rows * (uint64_t)ldx * 4u < 0xFFFFFFF0ull;
 #define SM_PANEL(GG)                                                                         \
     case GG:                                                                                 \
-        hipLaunchKernelGGL(spmm_rowpanel_kernel<GG>, dim3(grid), dim3(256), 0, s, n, nrhs, rp, \
-                           col, val, X, ldx, Y, ldy, alpha, beta);                            \
+        if (pipelined)                                                                       \
+            hipLaunchKernelGGL(spmm_rowpanel2_kernel<(GG <= 16 ? GG : 16)>, dim3(grid), dim3(256), 0, s, \
+                               n, nrhs, rp, col, val, nnz, X, ldx, x_rows, Y, ldy, alpha, beta); \
+        else                                                                                 \
+            hipLaunchKernelGGL(spmm_rowpanel_kernel<GG>, dim3(grid), dim3(256), 0, s, n, nrhs, rp, \
+                               col, val, X, ldx, Y, ldy, alpha, beta);                        \
         break;
     switch (G) {
         SM_PANEL(1) SM_PANEL(2) SM_PANEL(4) SM_PANEL(8) SM_PANEL(16) SM_PANEL(32)

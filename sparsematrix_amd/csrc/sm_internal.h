@@ -81,8 +81,9 @@ hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const
                                bool rhs_fastest, hipStream_t s);
 // Row-major X (k x nrhs, ldx) / Y (n x nrhs, ldy), nrhs % 4 == 0, 16-byte aligned.
 hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
-                                const float *val, const float *X, int64_t ldx, float *Y,
-                                int64_t ldy, float alpha, float beta, hipStream_t s);
+                                const float *val, int32_t nnz, const float *X, int64_t ldx,
+                                int64_t x_rows, float *Y, int64_t ldy, float alpha, float beta,
+                                hipStream_t s);
 hipError_t launch_beta(float *c, int32_t m, int32_t n, int64_t ldc, float beta, hipStream_t s);
 hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, float *sa,
                             int64_t ldsa, hipStream_t s);

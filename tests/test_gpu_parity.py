@@ -202,6 +202,34 @@ def test_spmm_n32_vs_oracle(sm):
         assert np.array_equal(bits(to_host(Yp)[:, :N2]), bits(want2)), N2
 
 
+@pytest.mark.parametrize("old", ["0", "1"])
+def test_spmm_ragged_all_panel_widths(sm, old):
+    """Row panels of every width (N = 4 .. 128, G = 1 .. 32 lanes per row) on ragged
+    rows (empty, shorter and longer than one 16-term group), with signed zeros;
+    SM_SPMM_OLD=1 runs the one-group-at-a-time kernel, 0 the gather-pipelined one
+    (kernels.hip).  Bit-exact against the oracle."""
+    n_rows, n_cols = 3000, 5000
+    rng = np.random.default_rng(21)
+    lengths = rng.integers(0, 41, n_rows)
+    lengths[::7] = 0
+    lengths[1::11] = 16
+    lengths[2::13] = 17
+    rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=22)
+    va[::5] = -0.0
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    for N in (4, 8, 16, 32, 64, 128):
+        X = rng.uniform(-1, 1, (n_cols, N)).astype(np.float32)
+        X[::3] = 0.0
+        X[1::9] = -0.0
+        Y0 = rng.uniform(-1, 1, (n_rows, N)).astype(np.float32)
+        Y0[::4] = -0.0
+        for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (-2.0, 0.0)):
+            want = oracle.csr_spmm(rp.astype(np.int64), ci, va, X, Y0, alpha, beta)
+            Y = to_dev(Y0)
+            _with_env("SM_SPMM_OLD", old, lambda: M.spmm(to_dev(X), Y, alpha, beta))
+            assert bits_equal(to_host(Y), want), (N, alpha, beta)
+
+
 # ---------------------------------------------------------------------------- edge cases
 def test_semantics_alpha_zero_beta_zero_nan(sm):
     rp, ci, va = uniform_csr(1000, 1000, 5, seed=1)
