@@ -11,8 +11,9 @@
 // no atomics).  Inside a tile a row's terms are therefore added in ascending
 // column order (bands ascend, ranks ascend inside a band).
 //
-// Slab 0 starts from beta*y and writes y; slab s > 0 starts from 0 and writes
-// partials[s-1].  The last tile of a row block to finish (a ticket counter per
+// Slab 0 starts from beta*y and writes y; slab s > 0 starts from -0.0 (the exact
+// identity of fp32 addition: a row without terms in the slab keeps the sign of a
+// zero y) and writes partials[s-1].  The last tile of a row block to finish (a ticket counter per
 // block) adds the partials to y in slab order -- the same sum whichever tile
 // finishes last.  The hand-off crosses CUs and XCDs: the slab sums are stored
 // write-through (sc1) and drained before the ticket, and the last tile reads
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     } else {
 #pragma unroll
         for (int q = 0; q < kQ; ++q)
-            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
     // Prologue: the loads the loop expects in flight, issued in its order
     // (per band q: slice q+kDmaAhead, then entries q+kEAhead).

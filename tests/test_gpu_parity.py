@@ -510,6 +510,31 @@ def test_xband_special_values(sm, kind):
             assert_terms_close(got[fin], want[fin], absum[fin])
 
 
+def test_xband_blocked_signed_zeros(sm):
+    """Blocked layout: a row whose terms are all -0.0 and whose y is -0.0 stays -0.0
+    across slabs (slab partials start from -0.0, the exact identity of fp32 addition);
+    rows without terms in a slab keep beta*y bit-for-bit."""
+    n_rows, n_cols = 40000, 200000
+    rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=79)
+    va = va.copy()
+    va[6 * 100:6 * 200] = -0.0
+    M = _with_env("SM_XBAND_KIND", "blocked", lambda: _with_env(
+        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    assert M.info()["has_xband"] == 2 and M.info()["xband_slabs"] > 1, M.info()
+    rng = np.random.default_rng(10)
+    x = rng.uniform(0.25, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    y0[:300] = -0.0
+    for alpha, beta in ((1.0, 1.0), (0.5, 0.0), (2.0, 3.0)):
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, alpha, beta, algo="xband")
+        got = to_host(y)
+        assert_terms_close(got, want, absum)
+        assert np.array_equal(bits(got[100:200]), bits(want[100:200]))   # -0.0 exactly
+
+
 def test_xband_not_applicable_falls_back(sm):
     """A row with more terms inside one band than the rank field holds cannot use the
     layout: the matrix is still served (stream kernel) and results stay correct;
