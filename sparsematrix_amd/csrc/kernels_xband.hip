@@ -30,6 +30,7 @@
 #include "xband.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace smamd {
 namespace {
@@ -78,14 +79,16 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
 // the x slice loads, bit 4 the entry loads, bit 16 the per-band barrier; the staged
 // slices are kept live so nothing upstream is dead-code removed; bit 128 skips the
 // slice stores into LDS (the loaded values kept live), 256 the whole band loop, 512
-// the slab hand-off and combine (plain stores instead), 2048 everything (launch cost).  Bit 32 records
+// the slab hand-off and combine (plain stores instead), 2048 everything (launch cost), 4096 the
+// value loads (word loads kept: half the entry bytes).  Bit 32 records
 // s_memtime stamps (tile 0, 6 per band per wave, bands < 32) into y[0, 3072).
 // Timing only: results are wrong.
 // XR: x slices held in registers (2 or 4): slice p+XR+(XR==2) is loaded at band p and
 // stored XR-1+(XR==2) bands later -- a deeper ring hides more L2 latency per band.
 // XR == 0: no register ring -- slices go HBM/L2 -> LDS directly (LDS-DMA) into a
 // ring of three LDS buffers, slice p+2 issued at band p.
-template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int XR, int ABL = 0>
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int XR, int ABL = 0,
+          bool STAGGER = true>
 __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
     int32_t slab_bands, const int32_t *__restrict__ chunk_start,
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
             uint32_t wl = ((uint32_t)(lane * 131) & kColMask) ^ kDummyWord, vl = off;
             if (!(ABL & 4)) {
                 wl = __builtin_amdgcn_raw_buffer_load_b32(w_src, off, 0, kAuxNt);
-                vl = __builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, kAuxNt);
+                if (!(ABL & 4096)) vl = __builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, kAuxNt);
             }
             w[k] = wl;
             v[k] = __uint_as_float(vl);
@@ -383,36 +386,52 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         const uint64_t t = __builtin_amdgcn_s_memtime();
         if (lane == 0) reinterpret_cast<uint32_t *>(y)[wave * 192 + p * 6 + k] = (uint32_t)t;
     };
-    auto step = [&](int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va, uint32_t *wl,
-                    float *vl) {
+    // LATE (waves >= kWaves/2 when STAGGER): apply first, then issue the band's
+    // loads -- so one half of the waves fills the TA queue while the other half
+    // works the LDS, instead of all 16 doing each in lockstep after the barrier.
+    // Same issue order per band in both roles, so the vmcnt plan is unchanged.
+    auto step = [&](auto late, int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va,
+                    uint32_t *wl, float *vl) {
+        constexpr bool kLate = decltype(late)::value;
         stamp(p, 0);
         if (p + kEAhead >= cw + 64) advance_cs_window();   // reads cs[p+A], cs[p+A+1]
-        if constexpr (kDma) {
-            // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
-            dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
-            stamp(p, 1);
-        } else {
-            store_slice((p + 1) & 1, xst);
-            stamp(p, 1);
-            load_slice(p + kXAhead, xld);
-        }
-        load_entries(p + kEAhead, wl, vl);
-        stamp(p, 2);
-        if (tracing) {
+        auto issue = [&]() {
+            if constexpr (kDma) {
+                // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
+                dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
+                stamp(p, 1);
+            } else {
+                store_slice((p + 1) & 1, xst);
+                stamp(p, 1);
+                load_slice(p + kXAhead, xld);
+            }
+            load_entries(p + kEAhead, wl, vl);
+            stamp(p, 2);
+        };
+        auto work = [&]() {
+            if (tracing) {
 #pragma unroll
-            for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
-            stamp(p, 3);
-        }
-        // Every chunk of the band is in registers: the builder guarantees at
-        // most CAP chunks per wave per band (no loop of loads in the pipeline,
-        // so hipcc can count vmcnt exactly).
-        if (ABL & 1) {
+                for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+                stamp(p, 3);
+            }
+            // Every chunk of the band is in registers: the builder guarantees at
+            // most CAP chunks per wave per band (no loop of loads in the pipeline,
+            // so hipcc can count vmcnt exactly).
+            if (ABL & 1) {
 #pragma unroll
-            for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+                for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+            } else {
+                apply_band(xs[kDma ? p % kXBufs : p & 1], wa, va);
+            }
+            stamp(p, 4);
+        };
+        if constexpr (kLate) {
+            work();
+            issue();
         } else {
-            apply_band(xs[kDma ? p % kXBufs : p & 1], wa, va);
+            issue();
+            work();
         }
-        stamp(p, 4);
         if constexpr (kDma) wait_vmcnt<kDmaWait>();   // slice p+1 landed (entries may fly)
         if (!(ABL & 16)) __syncthreads();
         stamp(p, 5);
@@ -422,16 +441,25 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // break paths into the loop header (tight waits in the first step).  Steps
     // past the tile's last band see only dummy entries and apply nothing.
     const int32_t nbu = (ABL & 256) ? 0 : (nb + kER - 1) / kER * kER;
-    for (int32_t p = 0; p < nbu; p += kER) {
+    auto band_loop = [&](auto late) {
+        for (int32_t p = 0; p < nbu; p += kER) {
 #pragma unroll
-        for (int u = 0; u < kER; ++u) {
-            // x: store slice p+u+1 from X[(u+1) % XR]; load slice p+u+kXAhead into the
-            // slot freed last (XR 4: slice p+u's; XR 2: the one just stored).
-            float4 *xst = X[(u + 1) % kXR];
-            float4 *xld = X[(XR == 4 ? u : u + 1) % kXR];
-            step(p + u, xst, xld, W[u], V[u], W[(u + kEAhead) % kER], V[(u + kEAhead) % kER]);
+            for (int u = 0; u < kER; ++u) {
+                // x: store slice p+u+1 from X[(u+1) % XR]; load slice p+u+kXAhead into the
+                // slot freed last (XR 4: slice p+u's; XR 2: the one just stored).
+                float4 *xst = X[(u + 1) % kXR];
+                float4 *xld = X[(XR == 4 ? u : u + 1) % kXR];
+                step(late, p + u, xst, xld, W[u], V[u], W[(u + kEAhead) % kER],
+                     V[(u + kEAhead) % kER]);
+            }
         }
-    }
+    };
+    // Two whole copies of the loop (a branch inside it would merge the two roles'
+    // vmcnt states): waves 0..7 issue-then-apply, waves 8..15 apply-then-issue.
+    if (STAGGER && wave >= kWaves / 2)
+        band_loop(std::true_type{});
+    else
+        band_loop(std::false_type{});
     if (tracing) return;
     if (n_slabs == 1 || (ABL & 512)) {
         const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
@@ -539,8 +567,21 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
     constexpr int XRr = (1 << BAND_LOG2) / (4 * THREADS) <= 2 ? 4 : 2;
     const char *dma_env = getenv("SM_XBAND_DMA");
     const bool dma = XRr == 4 && !(dma_env && atoi(dma_env) == 0);
+    // SM_XBAND_STAGGER=0: every wave issue-then-apply (A/B comparison only).
+    static const bool stagger = [] {
+        const char *e = getenv("SM_XBAND_STAGGER");
+        return !(e && atoi(e) == 0);
+    }();
 #define SM_XBL(XR)                                                                              \
-    hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL>),          \
+    do {                                                                                        \
+        if (stagger) {                                                                          \
+            SM_XBL2(XR, true);                                                                  \
+        } else {                                                                                \
+            SM_XBL2(XR, false);                                                                 \
+        }                                                                                       \
+    } while (0)
+#define SM_XBL2(XR, ST)                                                                         \
+    hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL, ST>),      \
                        dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
                        xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
@@ -551,6 +592,7 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
         SM_XBL(XRr);
     }
 #undef SM_XBL
+#undef SM_XBL2
     return hipGetLastError();
 }
 
@@ -579,6 +621,8 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
         case 768: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 2048: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 2048>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         case 37: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 4096: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4096>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 4097: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4097>(xb, n_rows, n_cols, x, y, alpha, beta, s);
         default: return hipErrorInvalidValue;
         }
     }
