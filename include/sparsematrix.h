@@ -99,6 +99,9 @@ typedef struct sm_info {
     int32_t xband_slabs;        /* column slabs per row block (1: bit-identical) */
     int32_t xband_block_rows;   /* rows per block                              */
     int64_t device_bytes;       /* device memory held by the matrix            */
+    int32_t col_relabel;        /* 1: the stream SpMV gathers x through a column
+                                   relabeling by descending degree (skewed graphs) */
+    int32_t reserved;
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */

@@ -4,6 +4,7 @@
 // kernels of kernels.hip; there is no CPU compute path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -11,6 +12,7 @@
 #include <limits>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "encode.h"
 #include "sm_internal.h"
@@ -82,6 +84,9 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.xb.d_val);
     (void)hipFree(m->plan.xb.d_partials);
     (void)hipFree(m->plan.xb.d_tickets);
+    (void)hipFree(m->plan.d_perm);
+    (void)hipFree(m->plan.d_rcol);
+    (void)hipFree(m->plan.d_xperm);
     m->d_row_ptr = m->d_col = nullptr;
     m->d_val = nullptr;
     m->plan = Plan();
@@ -189,6 +194,55 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     return SM_OK;
 }
 
+// Column relabeling for the stream kernel.  SM_RELABEL=0 disables
+// it, SM_RELABEL=1 forces it; otherwise it is built when x is larger than an XCD's
+// L2 (>= 2^20 columns), no band layout serves the matrix, there are at least as many
+// terms as columns (the per-SpMV permutation of x is then cheap next to the
+// product), and the column degrees are skewed: the busiest 1/16 of the columns hold
+// >= 40 % of the terms (power-law graphs: R-MAT scale 24 has 87 % there).
+bool want_relabel_size(const sm_matrix *m) {
+    const char *e = getenv("SM_RELABEL");
+    if (e && atoi(e) == 0) return false;
+    if (m->nnz == 0 || m->n_cols == 0) return false;
+    if (e && atoi(e) == 1) return true;
+    return m->n_cols >= (1 << 20) && m->nnz >= m->n_cols && m->plan.xb.n_blocks == 0;
+}
+
+sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
+    const int64_t nc = m->n_cols, nnz = m->nnz;
+    std::vector<int32_t> deg((size_t)nc, 0);
+    for (int64_t e = 0; e < nnz; e++) deg[(size_t)col[e]]++;
+    // new -> old, by descending degree; ties keep the original order (counting sort).
+    int32_t dmax = 0;
+    for (int32_t d : deg) dmax = std::max(dmax, d);
+    std::vector<int64_t> start((size_t)dmax + 2, 0);
+    for (int32_t d : deg) start[(size_t)(dmax - d) + 1]++;
+    for (size_t i = 1; i < start.size(); i++) start[i] += start[i - 1];
+    std::vector<int32_t> perm((size_t)nc), rank((size_t)nc);
+    for (int64_t c = 0; c < nc; c++) {
+        const int64_t j = start[(size_t)(dmax - deg[(size_t)c])]++;
+        perm[(size_t)j] = (int32_t)c;
+        rank[(size_t)c] = (int32_t)j;
+    }
+    const char *env = getenv("SM_RELABEL");
+    if (!(env && atoi(env) == 1)) {
+        int64_t hot = 0;
+        for (int64_t j = 0; j < nc / 16; j++) hot += deg[(size_t)perm[(size_t)j]];
+        if ((double)hot < 0.4 * (double)nnz) return SM_OK;   // not skewed: no gain
+    }
+    std::vector<int32_t> rcol((size_t)nnz);
+    for (int64_t e = 0; e < nnz; e++) rcol[(size_t)e] = rank[(size_t)col[e]];
+    Plan &p = m->plan;
+    SM_TRY_HIP(dev_alloc(&p.d_perm, nc + 4, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_rcol, nnz + kPadElems, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_xperm, nc + 4, m->device_bytes));
+    SM_TRY_HIP(hipMemcpy(p.d_perm, perm.data(), (size_t)nc * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(p.d_rcol, rcol.data(), (size_t)nnz * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemset(p.d_rcol + nnz, 0, kPadElems * sizeof(int32_t)));
+    p.n_relabel = nc;
+    return SM_OK;
+}
+
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
     const int32_t tile = tile_nnz_setting();
@@ -260,6 +314,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     }
     sm_status st2 = upload_plan(m, rp);
     if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val);
+    if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     return st2;
 }
 
@@ -457,17 +512,19 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
         return fail(SM_ERR_INVALID_MATRIX, "device CSR failed validation (flags 0x%x)", flag);
     }
     st = upload_plan(m.get(), rp.data());
-    if (st == SM_OK && want_xband(m.get())) {
+    const bool xband = want_xband(m.get());
+    if (st == SM_OK && (xband || want_relabel_size(m.get()))) {
         std::vector<int32_t> ch((size_t)nnz);
         std::vector<float> vh((size_t)nnz);
         hipError_t e3 = hipSuccess;
         if (nnz) {
             e3 = hipMemcpy(ch.data(), m->d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost);
-            if (e3 == hipSuccess)
+            if (e3 == hipSuccess && xband)
                 e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
         }
-        st = e3 == hipSuccess ? upload_xband(m.get(), rp.data(), ch.data(), vh.data())
-                              : hip_fail(e3, "copy CSR for band layout");
+        st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR for band layout / relabeling");
+        if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data());
+        if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }
     *out = m.release();
@@ -495,6 +552,7 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->xband_slabs = m->plan.xb.n_blocks > 0 ? m->plan.xb.n_slabs : 0;
     info->xband_block_rows = m->plan.xb.block_rows;
     info->device_bytes = m->device_bytes;
+    info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     return SM_OK;
 }
 
@@ -602,8 +660,15 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         // fall through: no band layout (or unaligned x) -> stream kernel
         [[fallthrough]];
     case SM_ALGO_STREAM:
-        // Long-row partial sums live in the matrix (allocated at creation): SpMVs on
-        // one matrix with long rows must not run concurrently on different streams.
+        // Long-row partial sums (and the relabeled x) live in the matrix (allocated at
+        // creation): SpMVs on one matrix must not run concurrently on different streams.
+        if (m->plan.n_relabel > 0) {
+            e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
+            if (e == hipSuccess)
+                e = launch_spmv_stream(m->plan, m->d_row_ptr, m->plan.d_rcol, m->d_val,
+                                       m->plan.d_xperm, y, alpha, beta, m->plan.d_partials, s);
+            break;
+        }
         e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
                                m->plan.d_partials, s);
         break;

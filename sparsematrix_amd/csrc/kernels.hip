@@ -475,6 +475,20 @@ __global__ __launch_bounds__(256) void scatter_dense_kernel(int32_t n, const int
     }
 }
 
+// xp[i] = x[perm[i]]: 4 outputs per thread (one 16-byte load of perm, four
+// gathers in flight, one 16-byte store); the tail (n % 4) one by one.
+__global__ __launch_bounds__(256) void x_relabel_kernel(int64_t n, const int32_t *__restrict__ perm,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ xp) {
+    const int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+    if (i + 4 <= n) {
+        const int4 p = *reinterpret_cast<const int4 *>(perm + i);
+        *reinterpret_cast<float4 *>(xp + i) = make_float4(x[p.x], x[p.y], x[p.z], x[p.w]);
+    } else {
+        for (int64_t k = i; k < n; ++k) xp[k] = x[perm[k]];
+    }
+}
+
 inline unsigned blocks_for(int64_t work, int per = 256) {
     return (unsigned)((work + per - 1) / per);
 }
@@ -597,6 +611,14 @@ hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const in
                            const int32_t *col, int32_t *d_flag, hipStream_t s) {
     hipLaunchKernelGGL(validate_kernel, dim3(blocks_for((int64_t)n_rows + 1)), dim3(256), 0, s,
                        n_rows, n_cols, nnz, rp, col, d_flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_x_relabel(int64_t n, const int32_t *perm, const float *x, float *xp,
+                            hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(x_relabel_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, s, n, perm,
+                       x, xp);
     return hipGetLastError();
 }
 

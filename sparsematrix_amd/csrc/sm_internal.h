@@ -61,6 +61,13 @@ struct Plan {
     float *d_partials = nullptr;      // n_chunks long-row partial sums (one SpMV in flight)
     int32_t max_row_nnz = 0;
     double avg_row_nnz = 0.0;
+    // Column relabeling for the stream kernel (skewed column degrees):
+    // columns renumbered by descending number of terms, so the hot part of x is
+    // a dense prefix that stays in L2.  Terms keep their stored order (bit-identical).
+    int64_t n_relabel = 0;            // n_cols when built, else 0
+    int32_t *d_perm = nullptr;        // new column -> original column
+    int32_t *d_rcol = nullptr;        // relabeled col_idx (nnz + kPadElems, zero tail)
+    float *d_xperm = nullptr;         // x in the new numbering (one SpMV in flight)
 };
 
 // Host launchers (kernels.hip).  All return hipError_t of the launch.
@@ -71,6 +78,9 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               float beta, float *partials, hipStream_t s);
 hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
+// xp[i] = x[perm[i]], i < n.
+hipError_t launch_x_relabel(int64_t n, const int32_t *perm, const float *x, float *xp,
+                            hipStream_t s);
 hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
                               const float *val, const float *x, float *y, float alpha, float beta,
                               hipStream_t s);
