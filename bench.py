@@ -16,10 +16,12 @@ ranks' algorithmic bytes divided by the max-over-ranks step time.
 Algorithmic bytes per SpMV: 8*nnz + 4*(rows+1) + 4*cols + 8*rows.
 
 Also reported, on the same JSON line:
-  roofline      the SpMV alone: algorithmic bytes / mean SpMV time (HIP events
-                around each sm_spmv call on its stream: the band kernel and, for
-                the blocked layout, the slab combine) vs 8 TB/s; `traffic` from
-                rocprofv3 PMC (profiles/traffic_<workload>_<layout>.json).
+  roofline      the SpMV alone: algorithmic bytes / mean SpMV time vs 8 TB/s.  N=1:
+                HIP events around the replay of the captured graph of K SpMVs, on
+                the stream it runs on (so the time per SpMV includes the gaps
+                between kernels); N>1: HIP events around each sm_spmv call on its
+                stream.  `traffic` from rocprofv3 PMC
+                (profiles/traffic_<workload>_<layout>.json).
   cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C) on the same
                 matrix, over the box's CPU share (OpenMP, <= 16 threads; SURVEY
                 §8d B2) with the 1-thread figure inside; ~15 s of CPU work.
@@ -64,7 +66,7 @@ def cpu_model() -> str:
 LAYOUTS = {0: "stream", 1: "exact", 2: "blocked"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "exact": "spmv_xband_kernel (exact band layout)",
-           "blocked": "spmv_xband_kernel (blocked band layout) + combine_slabs_kernel"}
+           "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)"}
 
 
 def load_traffic(workload: str, layout: str):
@@ -90,6 +92,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
     ap.add_argument("--spmm-n", type=int, default=32)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="N=1: launch each timed step from Python instead of replaying the K "
+                         "steps as one captured HIP graph")
     args = ap.parse_args()
 
     import torch
@@ -141,20 +146,43 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    # N = 1: the K timed SpMVs are captured once into a HIP graph (capturing runs
+    # nothing) and replayed as one launch, so the timed region holds the kernels
+    # back to back with no Python / ctypes / per-call launch cost between them; HIP
+    # events bracket the whole region on the stream the kernels run on.  N > 1:
+    # every step (RCCL all-gather + SpMV) is launched eagerly, with events around
+    # each SpMV.
+    use_graph = world == 1 and not args.no_graph
+    graph = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(args.steps):
+                step(args.warmup + i)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, events[i])
+    if use_graph:
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+        t0 = time.perf_counter()
+        events[0][0].record()
+        graph.replay()
+        events[0][1].record()
+    else:
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i, events[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in events]
+    if use_graph:   # one region of K SpMVs: per-SpMV time incl. the gaps between kernels
+        kern_ms = [kern_ms[0] / args.steps]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -248,7 +276,7 @@ def main():
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload, "rows_per_rank": R, "cols": C, "nnz_per_rank": nnz,
                        "per_row": per, "replicas": args.replicas, "algo": args.algo,
-                       "alpha": 1.0, "beta": 0.5,
+                       "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
                        "parallelism": f"row-partition x{world}" + (", RCCL all-gather(x)"
                                                                    if world > 1 else "")},
             "roofline": roof, "cpu_baseline": cpu, "spmm": spmm,

@@ -152,7 +152,10 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     const int threads = kXbThreads;
     const int64_t target_tiles = (int64_t)kXbTargetTiles * (kXbThreads / threads);   // fill the CUs
     XbandHost xh;
-    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, threads / 64, xh))
+    // Register capacity from the waves that hold entries: 12 on the blocked kind
+    // (4 loader waves stage x), all 16 on the exact kind.
+    const int entry_waves = kind == kXbExact ? threads / 64 : kXbComputeWaves;
+    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, entry_waves, xh))
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     XbandDev &d = m->plan.xb;
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.

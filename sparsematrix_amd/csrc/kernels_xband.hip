@@ -48,6 +48,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 constexpr int kAuxSc1 = 16; // write-through store / L1-bypassing load (cross-CU hand-off)
 
+// SM_XBAND_DMA=0: blocked x slices through a 4-slice register ring instead of LDS-DMA;
+// SM_XBAND_LOADERS=0/4/8: waves that only stage x (0: every wave stages and applies).  Both for A/B comparisons; read once.
+bool xband_dma_setting() {
+    static const bool on = [] {
+        const char *e = getenv("SM_XBAND_DMA");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+int xband_loaders_setting() {   // SM_XBAND_LOADERS = 0 (default), 4 or 8 loader waves
+    static const int n = [] {
+        const char *e = getenv("SM_XBAND_LOADERS");
+        const int v = e ? atoi(e) : 0;
+        return v == 4 || v == 8 ? v : 0;
+    }();
+    return n;
+}
+
 // vmcnt retires in issue order: waiting until only the N most recent vector loads
 // are outstanding retires every older one, including LDS-DMA that hipcc does not count.
 template <int N>
@@ -68,10 +86,13 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
         asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
     } else if constexpr (N == 3) {
         asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]));
-    } else {
-        static_assert(N == 4, "CAP of 1 to 4");
+    } else if constexpr (N == 4) {
         asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
                      "+v"(b[2]), "+v"(b[3]));
+    } else {
+        static_assert(N == 5, "CAP of 1 to 5");
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(b[0]),
+                     "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]));
     }
 }
 
@@ -88,7 +109,7 @@ __device__ __forceinline__ void pin_all(float *a, float *b) {
 // XR == 0: no register ring -- slices go HBM/L2 -> LDS directly (LDS-DMA) into a
 // ring of three LDS buffers, slice p+2 issued at band p.
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int XR, int ABL = 0,
-          bool STAGGER = true>
+          bool STAGGER = true, int LOADERS = 0>
 __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
     int32_t slab_bands, const int32_t *__restrict__ chunk_start,
@@ -117,6 +138,22 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
     // vmcnt at the end of band p that retires slice p+1 (issued kDmaAhead-1 bands
     // earlier, each band issuing its slice then its entries: 2*CAP loads).
     constexpr int kDmaWait = kDmaAhead == 2 ? 4 * CAP + kXv : 2 * CAP;
+    // LOADERS (LDS-DMA only, SM_XBAND_LOADERS=4|8, measured alternative): the last
+    // kLoaders waves only stage x (kPerLoader LDS-DMA pieces each per band, then a
+    // wait that retires nothing but x); the other kComp waves only load entries and
+    // apply.  Motivation: vmcnt retires in issue order, so a wave with entry loads in
+    // flight that waits for its x pieces also waits for every older entry load.
+    // Measured 49.2 us (4 or 8 loaders) vs 46.5 us without: a wave issues one 1 KiB
+    // LDS-DMA piece per ~150-190 cycles, so few loader waves serialise the x staging
+    // that 16 waves issue in parallel.  Default: 0 (every wave
+    // stages its share of x and applies).
+    constexpr bool kRoles = LOADERS > 0 && kDma;
+    constexpr int kLoaders = kRoles ? LOADERS : 0;
+    constexpr int kComp = kWaves - kLoaders;
+    constexpr int kPieces = BAND / 256;                 // 1 KiB LDS-DMA pieces per slice
+    constexpr int kPerLoader = kRoles ? kPieces / kLoaders : 1;
+    static_assert(!kRoles || (kPieces % (kRoles ? kLoaders : 1) == 0 && kXBufs == 3),
+                  "loader split");
     __shared__ __attribute__((aligned(16))) float xs[kXBufs][BAND];
     __shared__ float yacc[BROWS + kScratch];   // + one scratch slot per lane (writes that land nowhere)
     if (ABL & 2048) return;   // launch cost only
@@ -203,6 +240,25 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
                 : "memory");
         }
     };
+    // LOADERS: loader li = wave - kComp stages pieces li, li + kLoaders, ... of slice p.
+    auto dma_slice_loader = [&](int32_t p, int buf) {
+        const int li = wave - kComp;
+#pragma unroll
+        for (int k = 0; k < kPerLoader; ++k) {
+            const int m = k * kLoaders + li;
+            const uint32_t voff =
+                p < nb ? 4u * (uint32_t)(p * BAND + m * 256 + lane * 4) : 0xFFFFFFF0u;
+            const uint32_t lds =
+                __builtin_amdgcn_readfirstlane(xs_lds + 4u * (uint32_t)(buf * BAND + m * 256));
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(xr_src), "s"(lds)
+                : "memory");
+        }
+    };
     // Chunk c of band p for this wave.  A slot beyond the band's last chunk
     // loads from past the descriptor's range (no memory request, reads 0): words
     // are stored XOR the dummy word, so it is a dummy entry without a select
@@ -214,7 +270,7 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         const int32_t c1 = inb ? cs_at(p + 1) : 0;
 #pragma unroll
         for (int k = 0; k < CAP; ++k) {
-            const int32_t c = c0 + wave + k * kWaves;
+            const int32_t c = c0 + wave + k * kComp;
             const uint32_t off = c < c1 ? 4u * (uint32_t)(c * 64 + lane) : 0xFFFFFF00u;
             uint32_t wl = ((uint32_t)(lane * 131) & kColMask) ^ kDummyWord, vl = off;
             if (!(ABL & 4)) {
@@ -336,131 +392,185 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
         for (int q = 0; q < kQ; ++q)
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
-    // Prologue: the loads the loop expects in flight, issued in its order
-    // (per band q: slice q+kDmaAhead, then entries q+kEAhead).
-    if constexpr (kDma && kDmaAhead == 2) {   // pending after: E(A-2) D1 E(A-1)
-#pragma unroll
-        for (int q = 0; q <= kEAhead - 3; ++q) load_entries(q, W[q], V[q]);
-        dma_slice(0, 0);
-        load_entries(kEAhead - 2, W[kEAhead - 2], V[kEAhead - 2]);
-        dma_slice(1, 1);
-        load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
-        wait_vmcnt<kDmaWait>();   // slice 0 landed
-    } else if constexpr (kDma) {              // pending after: E(A-1)
-#pragma unroll
-        for (int q = 0; q <= kEAhead - 2; ++q) load_entries(q, W[q], V[q]);
-        dma_slice(0, 0);
-        load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
-        wait_vmcnt<kDmaWait>();   // slice 0 landed
-    } else if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
-        load_slice(0, X[0]);
-        load_slice(1, X[1]);
-        load_entries(0, W[0], V[0]);
-        load_slice(2, X[2 % kXR]);
-        load_entries(1, W[1], V[1]);
-        load_slice(3, X[3 % kXR]);
-        load_entries(2, W[2], V[2]);
-        store_slice(0, X[0]);
-    } else {                   // pending after: E0 X1 E1 X0 E2
-        load_slice(0, X[0]);
-        load_entries(0, W[0], V[0]);
-        load_slice(1, X[1 % kXR]);
-        load_entries(1, W[1], V[1]);
-        store_slice(0, X[0]);
-        load_slice(2, X[0]);
-        load_entries(2, W[2], V[2]);
-    }
-    __syncthreads();
-
-    // Band p (register staging): buffer p&1 holds slice p (visible); the ring holds
-    // slice p+1.  One barrier per band: the stores of slice p+1 into buffer (p+1)&1
-    // (freed by the previous barrier) and this band's reads of buffer p&1 both
-    // finish before it.  Slice p+kXAhead goes to the ring slot freed last (XR == 4:
-    // slice p's, stored a band ago; XR == 2: slice p+1's, stored just now).  LDS-DMA:
-    // slice p+kDmaAhead goes straight into the buffer freed by the last barrier.
-    // Entries of band p+kEAhead reuse the set of band p+kEAhead-kER.  Loads past the
-    // tile's last band are sent past the descriptors' ranges and never applied.
-    const bool tracing = (ABL & 32) && blockIdx.x == 0;
-    auto stamp = [&](int32_t p, int k) {
-        if (!tracing || p >= 32) return;
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        if (lane == 0) reinterpret_cast<uint32_t *>(y)[wave * 192 + p * 6 + k] = (uint32_t)t;
-    };
-    // LATE (waves >= kWaves/2 when STAGGER): apply first, then issue the band's
-    // loads -- so one half of the waves fills the TA queue while the other half
-    // works the LDS, instead of all 16 doing each in lockstep after the barrier.
-    // Same issue order per band in both roles, so the vmcnt plan is unchanged.
-    auto step = [&](auto late, int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va,
-                    uint32_t *wl, float *vl) {
-        constexpr bool kLate = decltype(late)::value;
-        stamp(p, 0);
-        if (p + kEAhead >= cw + 64) advance_cs_window();   // reads cs[p+A], cs[p+A+1]
-        auto issue = [&]() {
-            if constexpr (kDma) {
-                // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
-                dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
-                stamp(p, 1);
-            } else {
-                store_slice((p + 1) & 1, xst);
-                stamp(p, 1);
-                load_slice(p + kXAhead, xld);
-            }
-            load_entries(p + kEAhead, wl, vl);
-            stamp(p, 2);
+    if constexpr (kRoles) {
+        // Loaders: slices 0 and 1 in flight, slice 0 landed; then per band: slice
+        // p+2 into the buffer band p-1 freed, wait until only those pieces fly (slice
+        // p+1 landed), barrier.  Compute waves: entries 0..2 in flight; per band:
+        // entries p+3, apply band p, barrier.  One barrier per band in both roles.
+        const int32_t nbr = (ABL & 256) ? 0 : (nb + kER - 1) / kER * kER;
+        const bool rtrace = (ABL & 32) && blockIdx.x == 0;   // stamps (development only)
+        auto rstamp = [&](int32_t p, int k) {
+            if (!rtrace || p >= 32) return;
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) reinterpret_cast<uint32_t *>(y)[wave * 192 + p * 6 + k] = (uint32_t)t;
         };
-        auto work = [&]() {
-            if (tracing) {
-#pragma unroll
-                for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
-                stamp(p, 3);
+        if (wave >= kComp) {
+            dma_slice_loader(0, 0);
+            dma_slice_loader(1, 1);
+            wait_vmcnt<kPerLoader>();
+            __syncthreads();
+            for (int32_t p = 0; p < nbr; ++p) {
+                rstamp(p, 0);
+                dma_slice_loader(p + 2, (p + 2) % kXBufs);
+                rstamp(p, 1);
+                rstamp(p, 2);
+                wait_vmcnt<kPerLoader>();
+                rstamp(p, 3);
+                rstamp(p, 4);
+                __syncthreads();
+                rstamp(p, 5);
             }
-            // Every chunk of the band is in registers: the builder guarantees at
-            // most CAP chunks per wave per band (no loop of loads in the pipeline,
-            // so hipcc can count vmcnt exactly).
-            if (ABL & 1) {
-#pragma unroll
-                for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
-            } else {
-                apply_band(xs[kDma ? p % kXBufs : p & 1], wa, va);
-            }
-            stamp(p, 4);
-        };
-        if constexpr (kLate) {
-            work();
-            issue();
         } else {
-            issue();
-            work();
-        }
-        if constexpr (kDma) wait_vmcnt<kDmaWait>();   // slice p+1 landed (entries may fly)
-        if (!(ABL & 16)) __syncthreads();
-        stamp(p, 5);
-    };
-    // Whole groups of kER bands, no early exit: a break out of the unrolled body
-    // would share the loop latch and make hipcc's vmcnt bookkeeping merge the
-    // break paths into the loop header (tight waits in the first step).  Steps
-    // past the tile's last band see only dummy entries and apply nothing.
-    const int32_t nbu = (ABL & 256) ? 0 : (nb + kER - 1) / kER * kER;
-    auto band_loop = [&](auto late) {
-        for (int32_t p = 0; p < nbu; p += kER) {
 #pragma unroll
-            for (int u = 0; u < kER; ++u) {
-                // x: store slice p+u+1 from X[(u+1) % XR]; load slice p+u+kXAhead into the
-                // slot freed last (XR 4: slice p+u's; XR 2: the one just stored).
-                float4 *xst = X[(u + 1) % kXR];
-                float4 *xld = X[(XR == 4 ? u : u + 1) % kXR];
-                step(late, p + u, xst, xld, W[u], V[u], W[(u + kEAhead) % kER],
-                     V[(u + kEAhead) % kER]);
+            for (int q = 0; q < kEAhead; ++q) load_entries(q, W[q], V[q]);
+            __syncthreads();
+            for (int32_t p = 0; p < nbr; p += kER) {
+#pragma unroll
+                for (int u = 0; u < kER; ++u) {
+                    rstamp(p + u, 0);
+                    if (p + u + kEAhead >= cw + 64) advance_cs_window();
+                    rstamp(p + u, 1);
+                    load_entries(p + u + kEAhead, W[(u + kEAhead) % kER], V[(u + kEAhead) % kER]);
+                    rstamp(p + u, 2);
+                    if (rtrace) {
+#pragma unroll
+                        for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(W[u][k]), "v"(V[u][k]));
+                    }
+                    rstamp(p + u, 3);
+                    apply_band(xs[(p + u) % kXBufs], W[u], V[u]);
+                    rstamp(p + u, 4);
+                    __syncthreads();
+                    rstamp(p + u, 5);
+                }
             }
         }
-    };
-    // Two whole copies of the loop (a branch inside it would merge the two roles'
-    // vmcnt states): waves 0..7 issue-then-apply, waves 8..15 apply-then-issue.
-    if (STAGGER && wave >= kWaves / 2)
-        band_loop(std::true_type{});
-    else
-        band_loop(std::false_type{});
-    if (tracing) return;
+    } else {
+        // Prologue: the loads the loop expects in flight, issued in its order
+        // (per band q: slice q+kDmaAhead, then entries q+kEAhead).
+        if constexpr (kDma && kDmaAhead == 2) {   // pending after: E(A-2) D1 E(A-1)
+    #pragma unroll
+            for (int q = 0; q <= kEAhead - 3; ++q) load_entries(q, W[q], V[q]);
+            dma_slice(0, 0);
+            load_entries(kEAhead - 2, W[kEAhead - 2], V[kEAhead - 2]);
+            dma_slice(1, 1);
+            load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
+            wait_vmcnt<kDmaWait>();   // slice 0 landed
+        } else if constexpr (kDma) {              // pending after: E(A-1)
+    #pragma unroll
+            for (int q = 0; q <= kEAhead - 2; ++q) load_entries(q, W[q], V[q]);
+            dma_slice(0, 0);
+            load_entries(kEAhead - 1, W[kEAhead - 1], V[kEAhead - 1]);
+            wait_vmcnt<kDmaWait>();   // slice 0 landed
+        } else if constexpr (XR == 4) {   // pending after: X1 E0 X2 E1 X3 E2
+            load_slice(0, X[0]);
+            load_slice(1, X[1]);
+            load_entries(0, W[0], V[0]);
+            load_slice(2, X[2 % kXR]);
+            load_entries(1, W[1], V[1]);
+            load_slice(3, X[3 % kXR]);
+            load_entries(2, W[2], V[2]);
+            store_slice(0, X[0]);
+        } else {                   // pending after: E0 X1 E1 X0 E2
+            load_slice(0, X[0]);
+            load_entries(0, W[0], V[0]);
+            load_slice(1, X[1 % kXR]);
+            load_entries(1, W[1], V[1]);
+            store_slice(0, X[0]);
+            load_slice(2, X[0]);
+            load_entries(2, W[2], V[2]);
+        }
+        __syncthreads();
+
+        // Band p (register staging): buffer p&1 holds slice p (visible); the ring holds
+        // slice p+1.  One barrier per band: the stores of slice p+1 into buffer (p+1)&1
+        // (freed by the previous barrier) and this band's reads of buffer p&1 both
+        // finish before it.  Slice p+kXAhead goes to the ring slot freed last (XR == 4:
+        // slice p's, stored a band ago; XR == 2: slice p+1's, stored just now).  LDS-DMA:
+        // slice p+kDmaAhead goes straight into the buffer freed by the last barrier.
+        // Entries of band p+kEAhead reuse the set of band p+kEAhead-kER.  Loads past the
+        // tile's last band are sent past the descriptors' ranges and never applied.
+        const bool tracing = (ABL & 32) && blockIdx.x == 0;
+        auto stamp = [&](int32_t p, int k) {
+            if (!tracing || p >= 32) return;
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) reinterpret_cast<uint32_t *>(y)[wave * 192 + p * 6 + k] = (uint32_t)t;
+        };
+        // LATE (waves >= kWaves/2 when STAGGER): apply first, then issue the band's
+        // loads -- so one half of the waves fills the TA queue while the other half
+        // works the LDS, instead of all 16 doing each in lockstep after the barrier.
+        // Same issue order per band in both roles, so the vmcnt plan is unchanged.
+        auto step = [&](auto late, int32_t p, float4 *xst, float4 *xld, uint32_t *wa, float *va,
+                        uint32_t *wl, float *vl) {
+            constexpr bool kLate = decltype(late)::value;
+            stamp(p, 0);
+            if (p + kEAhead >= cw + 64) advance_cs_window();   // reads cs[p+A], cs[p+A+1]
+            auto issue = [&]() {
+                if constexpr (kDma) {
+                    // The buffer of slice p+kDmaAhead-kXBufs = p-1, freed by the last barrier.
+                    dma_slice(p + kDmaAhead, (p + kDmaAhead) % kXBufs);
+                    stamp(p, 1);
+                } else {
+                    store_slice((p + 1) & 1, xst);
+                    stamp(p, 1);
+                    load_slice(p + kXAhead, xld);
+                }
+                load_entries(p + kEAhead, wl, vl);
+                stamp(p, 2);
+            };
+            auto work = [&]() {
+                if (tracing) {
+    #pragma unroll
+                    for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+                    stamp(p, 3);
+                }
+                // Every chunk of the band is in registers: the builder guarantees at
+                // most CAP chunks per wave per band (no loop of loads in the pipeline,
+                // so hipcc can count vmcnt exactly).
+                if (ABL & 1) {
+    #pragma unroll
+                    for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(wa[k]), "v"(va[k]));
+                } else {
+                    apply_band(xs[kDma ? p % kXBufs : p & 1], wa, va);
+                }
+                stamp(p, 4);
+            };
+            if constexpr (kLate) {
+                work();
+                issue();
+            } else {
+                issue();
+                work();
+            }
+            if constexpr (kDma) wait_vmcnt<kDmaWait>();   // slice p+1 landed (entries may fly)
+            if (!(ABL & 16)) __syncthreads();
+            stamp(p, 5);
+        };
+        // Whole groups of kER bands, no early exit: a break out of the unrolled body
+        // would share the loop latch and make hipcc's vmcnt bookkeeping merge the
+        // break paths into the loop header (tight waits in the first step).  Steps
+        // past the tile's last band see only dummy entries and apply nothing.
+        const int32_t nbu = (ABL & 256) ? 0 : (nb + kER - 1) / kER * kER;
+        auto band_loop = [&](auto late) {
+            for (int32_t p = 0; p < nbu; p += kER) {
+    #pragma unroll
+                for (int u = 0; u < kER; ++u) {
+                    // x: store slice p+u+1 from X[(u+1) % XR]; load slice p+u+kXAhead into the
+                    // slot freed last (XR 4: slice p+u's; XR 2: the one just stored).
+                    float4 *xst = X[(u + 1) % kXR];
+                    float4 *xld = X[(XR == 4 ? u : u + 1) % kXR];
+                    step(late, p + u, xst, xld, W[u], V[u], W[(u + kEAhead) % kER],
+                         V[(u + kEAhead) % kER]);
+                }
+            }
+        };
+        // Two whole copies of the loop (a branch inside it would merge the two roles'
+        // vmcnt states): waves 0..7 issue-then-apply, waves 8..15 apply-then-issue.
+        if (STAGGER && wave >= kWaves / 2)
+            band_loop(std::true_type{});
+        else
+            band_loop(std::false_type{});
+    }
+    if ((ABL & 32) && blockIdx.x == 0) return;   // stamps only
     if (n_slabs == 1 || (ABL & 512)) {
         const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
 #pragma unroll
@@ -559,77 +669,79 @@ __global__ __launch_bounds__(THREADS) void spmv_xband_kernel(
 
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int ABL>
 hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
-                        float *y, float alpha, float beta, hipStream_t s) {
+                        float *y, float alpha, float beta, int loaders, hipStream_t s) {
     // x staging: blocked (2 float4 per thread per slice) by LDS-DMA into three LDS
-    // buffers (2.5 % faster than its 4-slice register ring, which SM_XBAND_DMA=0
-    // selects for comparison); exact (4 float4 per slice, no room for a third
-    // 64 KiB buffer) through a 2-slice register ring.
+    // buffers, issued by 4 loader waves (roles) or by every wave; exact (4 float4
+    // per slice, no room for a third 64 KiB buffer) through a 2-slice register ring.
     constexpr int XRr = (1 << BAND_LOG2) / (4 * THREADS) <= 2 ? 4 : 2;
-    const char *dma_env = getenv("SM_XBAND_DMA");
-    const bool dma = XRr == 4 && !(dma_env && atoi(dma_env) == 0);
-    // SM_XBAND_STAGGER=0: every wave issue-then-apply (A/B comparison only).
-    static const bool stagger = [] {
-        const char *e = getenv("SM_XBAND_STAGGER");
-        return !(e && atoi(e) == 0);
-    }();
-#define SM_XBL(XR)                                                                              \
-    do {                                                                                        \
-        if (stagger) {                                                                          \
-            SM_XBL2(XR, true);                                                                  \
-        } else {                                                                                \
-            SM_XBL2(XR, false);                                                                 \
-        }                                                                                       \
-    } while (0)
-#define SM_XBL2(XR, ST)                                                                         \
-    hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL, ST>),      \
+    const bool dma = XRr == 4 && xband_dma_setting();
+#define SM_XBL(XR, RL)                                                                          \
+    hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, XR, ABL, true, RL>), \
                        dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
                        xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
                        alpha, beta)
     if (dma) {
-        if constexpr (XRr == 4) SM_XBL(0);
+        if constexpr (XRr == 4) {
+            if (loaders == 8)
+                SM_XBL(0, 8);
+            else if (loaders == 4)
+                SM_XBL(0, 4);
+            else
+                SM_XBL(0, 0);
+        }
     } else {
-        SM_XBL(XRr);
+        SM_XBL(XRr, 0);
     }
 #undef SM_XBL
-#undef SM_XBL2
     return hipGetLastError();
 }
 
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2>
 hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                        float *y, float alpha, float beta, hipStream_t s) {
-    const int waves = THREADS / 64;
-    const int64_t cap = (xb.max_chunks_per_band + waves - 1) / waves;
     const char *abl_env = getenv("SM_XBAND_ABLATE");   // development only
     const int abl = abl_env ? atoi(abl_env) : 0;
+    // Loader waves on the LDS-DMA path (SM_XBAND_LOADERS, default none; a count whose
+    // applying waves would need more than kXbMaxCap chunks per band is halved).
+    constexpr bool kDmaKind = (1 << BAND_LOG2) / (4 * THREADS) <= 2;
+    int loaders = kDmaKind && (abl == 0 || abl == 32) && xband_dma_setting()
+                      ? xband_loaders_setting() : 0;
+    auto cap_for = [&](int ld) {   // chunks per applying wave per band
+        const int waves = THREADS / 64 - ld;
+        return (xb.max_chunks_per_band + waves - 1) / waves;
+    };
+    while (loaders > 0 && cap_for(loaders) > kXbMaxCap) loaders /= 2;   // 8 -> 4 -> 2 -> 1 -> 0
+    if (loaders != 8 && loaders != 4) loaders = 0;
+    const int64_t cap = cap_for(loaders);
+#define SM_XBT(C, A) launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, C, A>(xb, n_rows, n_cols, x, y, alpha, beta, loaders, s)
     if (abl) {
-        if (cap > kXbMaxCap) return hipErrorInvalidValue;
+        if (cap > 4) return hipErrorInvalidValue;
         switch (abl) {
-        case 1: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 1>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 2: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 4: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 5: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 5>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 16: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 16>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 32: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 32>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 133: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 133>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 21: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 21>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 149: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 149>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 7: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 7>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 256: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 256>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 512: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 512>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 768: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 768>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 2048: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 2048>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 37: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 37>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 4096: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4096>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-        case 4097: return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 4097>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+        case 1: return SM_XBT(4, 1);
+        case 2: return SM_XBT(4, 2);
+        case 4: return SM_XBT(4, 4);
+        case 5: return SM_XBT(4, 5);
+        case 16: return SM_XBT(4, 16);
+        case 32: return SM_XBT(4, 32);
+        case 21: return SM_XBT(4, 21);
+        case 7: return SM_XBT(4, 7);
+        case 256: return SM_XBT(4, 256);
+        case 512: return SM_XBT(4, 512);
+        case 768: return SM_XBT(4, 768);
+        case 2048: return SM_XBT(4, 2048);
+        case 37: return SM_XBT(4, 37);
+        case 4096: return SM_XBT(4, 4096);
+        case 4097: return SM_XBT(4, 4097);
         default: return hipErrorInvalidValue;
         }
     }
-    if (cap <= 1) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 1, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= 2) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 2, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= 3) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 3, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
-    if (cap <= kXbMaxCap) return launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, 4, 0>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    if (cap <= 1) return SM_XBT(1, 0);
+    if (cap <= 2) return SM_XBT(2, 0);
+    if (cap <= 3) return SM_XBT(3, 0);
+    if (cap <= 4) return SM_XBT(4, 0);
+    if (cap <= kXbMaxCap) return SM_XBT(5, 0);
+#undef SM_XBT
     return hipErrorInvalidValue;
 }
 

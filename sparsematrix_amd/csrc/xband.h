@@ -30,7 +30,8 @@ constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbThreads = 1024;               // one workgroup per CU
 constexpr int kXbMaxBands = 4096;              // n_cols <= 32 M (blocked) / 64 M (exact)
-constexpr int kXbMaxCap = 4;                   // chunks per wave per band held in registers
+constexpr int kXbMaxCap = 5;                   // chunks per wave per band held in registers
+constexpr int kXbComputeWaves = 12;            // blocked kind: waves that apply (4 stage x)
 constexpr int kXbTargetTiles = 256;            // blocked: >= one tile per CU
 
 struct XbandHost {

@@ -101,6 +101,16 @@ class SparseMatrix:
             raise RuntimeError("SparseMatrix is empty (call CopyForm or from_csr first)")
         return self._h
 
+    def _dims(self):
+        """(n_rows, n_cols) of the held matrix, cached per handle: the per-call operand
+        guards of spmv/spmm then cost no sm_get_info round trip."""
+        h = self._require()
+        if getattr(self, "_dims_h", None) != h:
+            inf = self.info()
+            self._dims_cache = (inf["n_rows"], inf["n_cols"])
+            self._dims_h = h
+        return self._dims_cache
+
     # ---- construction -----------------------------------------------------
     def CopyForm(self, density_matrix, rows: int, cols: int, stride: int, vals,
                  val_table_size: int, trans: int = SblasNoTrans) -> None:
@@ -250,9 +260,9 @@ class SparseMatrix:
 
     def spmv(self, x, y, alpha: float = 1.0, beta: float = 1.0, algo="auto", stream=None):
         """y = alpha * B * x + beta * y on device tensors (float32, contiguous)."""
-        inf = self.info()
-        _check_dev(x, inf["n_cols"], "x")
-        _check_dev(y, inf["n_rows"], "y")
+        n_rows, n_cols = self._dims()
+        _check_dev(x, n_cols, "x")
+        _check_dev(y, n_rows, "y")
         if (x.dim() != 1 and not x.is_contiguous()) or (y.dim() != 1 and not y.is_contiguous()):
             raise ValueError("x and y must be contiguous")
         if x.dim() == 1 and x.stride(0) != 1 or y.dim() == 1 and y.stride(0) != 1:
@@ -265,9 +275,9 @@ class SparseMatrix:
     def spmm(self, X, Y, alpha: float = 1.0, beta: float = 1.0, algo="auto", stream=None):
         """Y (n x N) = alpha * B * X (k x N) + beta * Y, row-major device tensors."""
         n_rhs = int(Y.shape[1])
-        inf = self.info()
-        _check_dev_2d(X, inf["n_cols"], n_rhs, "X")
-        _check_dev_2d(Y, inf["n_rows"], n_rhs, "Y")
+        n_rows, n_cols = self._dims()
+        _check_dev_2d(X, n_cols, n_rhs, "X")
+        _check_dev_2d(Y, n_rows, n_rhs, "Y")
         st = self._L.sm_spmm(self._require(), n_rhs, alpha, _ptr(X), int(X.stride(0)), beta,
                              _ptr(Y), int(Y.stride(0)), _algo(algo), _stream_of(Y, stream))
         check(st, "sm_spmm")

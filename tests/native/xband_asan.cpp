@@ -82,7 +82,7 @@ int main() {
     const XbBits blocked = xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
     int bad = 0;
     const struct { XbBits bits; int waves; } kinds[] = {
-        {exact, kXbThreads / 64}, {blocked, kXbThreads / 64}};
+        {exact, kXbThreads / 64}, {blocked, kXbComputeWaves}};
     for (const auto &k : kinds) {
         bad += check(k.bits, k.waves, 200003, 300001, 16, 1, true);
         bad += check(k.bits, k.waves, 9000, 70001, 40, 2, true);    // dense bands: smaller blocks
