@@ -63,10 +63,11 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-LAYOUTS = {0: "stream", 1: "exact", 2: "blocked"}
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "exact": "spmv_xband_kernel (exact band layout)",
-           "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)"}
+           "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)",
+           "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)"}
 
 
 def load_traffic(workload: str, layout: str):

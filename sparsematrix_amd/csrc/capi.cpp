@@ -129,6 +129,7 @@ int32_t tile_nnz_setting() {
 XbKind xband_kind_setting() {
     const char *e = getenv("SM_XBAND_KIND");
     if (e && strcmp(e, "exact") == 0) return kXbExact;
+    if (e && strcmp(e, "gather") == 0) return kXbGather;
     return kXbBlocked;
 }
 
@@ -138,24 +139,28 @@ bool want_xband(const sm_matrix *m) {
     if (m->nnz == 0 || m->n_rows == 0) return false;
     if (e && atoi(e) == 1) return true;
     const XbKind kind = xband_kind_setting();
-    const int rows_log2 = kind == kXbExact ? kXbExactRowsLog2 : kXbBlockedRowsLog2;
+    const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
+                          : kind == kXbGather ? kXbGatherRowsLog2
+                                              : kXbBlockedRowsLog2;
     const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
     const double x_sweep = (double)nblk * 4.0 * (double)m->n_cols;   // L2 -> LDS bytes
     const double stream = 8.0 * (double)m->nnz;                      // HBM bytes
     return x_sweep <= 20.0 * stream && m->n_cols >= 8192;
 }
 
-sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
-    const XbKind kind = xband_kind_setting();
-    const XbBits bits = kind == kXbExact ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
-                                         : xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
+sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
+                       XbKind kind) {
+    const XbBits bits = kind == kXbExact    ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
+                        : kind == kXbGather ? xb_bits(kXbGatherBandLog2, kXbGatherRowsLog2)
+                                            : xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
     const int threads = kXbThreads;
     const int64_t target_tiles = (int64_t)kXbTargetTiles * (kXbThreads / threads);   // fill the CUs
     XbandHost xh;
     // Register capacity from the waves that hold entries: 12 on the blocked kind
-    // (4 loader waves stage x), all 16 on the exact kind.
-    const int entry_waves = kind == kXbExact ? threads / 64 : kXbComputeWaves;
-    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, entry_waves, xh))
+    // (4 loader waves stage x), all 16 on the exact and gather kinds.
+    const int entry_waves = kind == kXbBlocked ? kXbComputeWaves : threads / 64;
+    if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, entry_waves, xh,
+                     kind == kXbGather))
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     XbandDev &d = m->plan.xb;
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
@@ -316,7 +321,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
         SM_TRY_HIP(hipMemcpy(m->d_val, val, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
     }
     sm_status st2 = upload_plan(m, rp);
-    if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val);
+    if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting());
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     return st2;
 }
@@ -526,7 +531,7 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
                 e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
         }
         st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR for band layout / relabeling");
-        if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data());
+        if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting());
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }

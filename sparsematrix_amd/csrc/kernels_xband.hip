@@ -30,6 +30,7 @@
 #include "xband.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace smamd {
@@ -745,6 +746,360 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
     return hipErrorInvalidValue;
 }
 
+
+// ---------------------------------------------------------------------------
+// Gather-band kernel (kind kXbGather).  Same tiles, chunks,
+// rank rounds, slab hand-off and summation order as the kernel above, but x is
+// not staged through LDS: the builder lists a band's segments by first column,
+// so the 64 x gathers of one wave-instruction fall in a window of ~1 KiB (about
+// 8 lanes per 128-byte line at 16 terms per row), which the TA coalesces --
+// windowed gathers run at the index-stream rate (profiles/r01_microbench.txt)
+// while fully random ones are TA-bound.  Per band a wave loads the entries of
+// band p+EA, gathers the x values of band p+GA (their words arrived EA-GA
+// bands ago) and applies band p: only the accumulator read and write touch LDS,
+// no x slice is stored and LDS holds nothing but the accumulators.  One barrier
+// per band keeps a row's terms in ascending column order.  Measured slower than
+// the LDS-staged kernel on config 2 (54 vs 48 us): the gathers and
+// the apply each add ~10 us that do not overlap the entry stream; 32K-row blocks
+// (half the x per term) pay more in their 8-slab hand-off than they save.
+template <int N>
+__device__ __forceinline__ void pin_one(float *a) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) asm volatile("" : "+v"(a[k]));
+}
+
+// ABL (development only, SM_GBAND_ABLATE; results wrong): 1 skips the x gathers,
+// 2 the apply (loaded values kept live), 4 the slab hand-off (plain stores).
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP, int EA, int GA, int ABL = 0>
+__global__ __launch_bounds__(THREADS) void spmv_gband_kernel(
+    int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_bands, int32_t n_slabs,
+    int32_t slab_bands, const int32_t *__restrict__ chunk_start,
+    const uint32_t *__restrict__ word, const float *__restrict__ val,
+    const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
+    int32_t *__restrict__ tickets, float alpha, float beta) {
+    constexpr int BAND = 1 << BAND_LOG2;
+    constexpr int BROWS = 1 << ROWS_LOG2;
+    constexpr XbBits kBits = xb_bits(BAND_LOG2, ROWS_LOG2);
+    constexpr uint32_t kColMask = (1u << kBits.col) - 1u;
+    constexpr uint32_t kRankMask = (1u << kBits.rank) - 1u;
+    constexpr uint32_t kDummyRank = kBits.dummy_rank();
+    constexpr uint32_t kDummyWord = kBits.dummy_word();
+    constexpr int kWaves = THREADS / 64;
+    constexpr int kER = EA < 4 ? 4 : 8;   // entry ring = loop unroll
+    constexpr int kXR = GA < 4 ? 4 : 8;   // x-value ring
+    static_assert(GA >= 1 && GA < EA && EA < kER && kER % kXR == 0, "lookaheads");
+    static_assert(BROWS % (4 * THREADS) == 0, "accumulator init in float4 per thread");
+    __shared__ __attribute__((aligned(16))) float yacc[BROWS + 64];   // + a scratch slot per lane
+    __shared__ int32_t s_ticket;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int32_t b = blockIdx.x / n_slabs;
+    const int32_t slab = blockIdx.x - b * n_slabs;
+    const int32_t p_first = slab * slab_bands;
+    const int32_t nb = min(slab_bands, n_bands - p_first);
+    const int32_t r0 = b * block_rows;
+    const int32_t nr = min(block_rows, n_rows - r0);
+    const int32_t *csg = chunk_start + (int64_t)b * n_bands + p_first;
+    const int32_t c_first = csg[0];
+    const int32_t c_last = csg[nb];
+    const int64_t x0 = (int64_t)p_first * BAND;
+    const __amdgpu_buffer_rsrc_t xr_src = rsrc(x + x0, (uint64_t)(n_cols - x0) * 4);
+    const __amdgpu_buffer_rsrc_t w_src =
+        rsrc(word + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
+    const __amdgpu_buffer_rsrc_t v_src =
+        rsrc(val + (int64_t)c_first * 64, (uint64_t)(c_last - c_first) * 256);
+    // Chunk table window in registers (as above).
+    int32_t cw = 0;
+    int32_t cs_lo = csg[min(lane, nb)];
+    int32_t cs_hi = csg[min(64 + lane, nb)];
+    auto advance_cs_window = [&]() {
+        cw += 64;
+        cs_lo = cs_hi;
+        cs_hi = csg[min(cw + 64 + lane, nb)];
+    };
+    auto cs_at = [&](int32_t i) -> int32_t {
+        const int32_t j = i - cw;
+        const int32_t lo = __builtin_amdgcn_readlane(cs_lo, j & 63);
+        const int32_t hi = __builtin_amdgcn_readlane(cs_hi, j & 63);
+        return (j < 64 ? lo : hi) - c_first;
+    };
+    // Chunk c0+wave+16k of band p; slots past the band read 0 = a dummy (see above).
+    auto load_entries = [&](int32_t p, uint32_t *w, float *v) {
+        const bool inb = p < nb;
+        const int32_t c0 = inb ? cs_at(p) : 0;
+        const int32_t c1 = inb ? cs_at(p + 1) : 0;
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            const int32_t c = c0 + wave + k * kWaves;
+            const uint32_t off = c < c1 ? 4u * (uint32_t)(c * 64 + lane) : 0xFFFFFF00u;
+            w[k] = __builtin_amdgcn_raw_buffer_load_b32(w_src, off, 0, kAuxNt);
+            v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(v_src, off, 0, kAuxNt));
+        }
+    };
+    // x values of band p's entries (dummies decode to column 0 of the band: a
+    // harmless in-range read; bands past the tile read nothing).
+    auto gather_x = [&](int32_t p, const uint32_t *w, float *xg) {
+        const uint32_t pb = p < nb ? (uint32_t)p * BAND : 0u;
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            const uint32_t col = (w[k] ^ kDummyWord) & kColMask;
+            const uint32_t off = p < nb ? 4u * (pb + col) : 0xFFFFFF00u;
+            if (ABL & 1)
+                xg[k] = __uint_as_float(off);
+            else
+                xg[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr_src, off, 0, 0));
+        }
+    };
+    auto shr1 = [](float v) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+    };
+    auto shl1 = [](uint32_t v) {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)kDummyRank, (int)v, 0x130, 0xF, 0xF, false);
+    };
+    auto apply_band = [&](const float *xv, const uint32_t *wa, const float *va) {
+        float yv[CAP];
+        uint32_t rk[CAP], rl[CAP];
+        bool live[CAP];
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            const uint32_t wd = wa[k] ^ kDummyWord;
+            rk[k] = (wd >> kBits.col) & kRankMask;
+            live[k] = rk[k] != kDummyRank;
+            rl[k] = wd >> (kBits.col + kBits.rank);
+            yv[k] = yacc[rl[k]];
+            more |= live[k] && rk[k] > 0;
+        }
+        pin_one<CAP>(yv);
+        float t[CAP], acc[CAP];
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            t[k] = __fmul_rn(xv[k], __fmul_rn(va[k], alpha));
+            acc[k] = __fadd_rn(yv[k], t[k]);
+        }
+        if (__any(more)) {
+            for (uint32_t r = 1;; ++r) {
+                bool again = false;
+#pragma unroll
+                for (int k = 0; k < CAP; ++k) {
+                    const float prev = shr1(acc[k]);
+                    if (rk[k] == r) acc[k] = __fadd_rn(prev, t[k]);
+                    again |= live[k] && rk[k] > r;
+                }
+                if (!__any(again)) break;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CAP; ++k) {
+            const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
+            yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
+        }
+    };
+
+    // Accumulators: beta*y (slab 0) or -0.0 (see above), all loads in flight at once.
+    constexpr int kQ = BROWS / (4 * THREADS);
+    const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
+    if (slab == 0) {
+        const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
+        float4 v[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint32_t o = 16u * (uint32_t)(tid + q * THREADS);
+            if (y_vec) {
+                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(yi_src, o, 0, 0);
+                v[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                   __uint_as_float(u.z), __uint_as_float(u.w));
+            } else {
+                v[q] = make_float4(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 4, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 8, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 12, 0, 0)));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (beta != 1.0f)
+                v[q] = make_float4(__fmul_rn(v[q].x, beta), __fmul_rn(v[q].y, beta),
+                                   __fmul_rn(v[q].z, beta), __fmul_rn(v[q].w, beta));
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = v[q];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * THREADS)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
+    }
+
+    // Rings with static roles: entries of band q in W/V[q % kER], its x values in
+    // XG[q % kER].  Prologue: the loads the loop expects in flight, in its order
+    // (band q issues entries q+EA, then gathers q+GA).
+    uint32_t W[kER][CAP];
+    float V[kER][CAP];
+    float XG[kXR][CAP];
+#pragma unroll
+    for (int q = -EA; q < 0; ++q) {
+        load_entries(q + EA, W[(q + EA) % kER], V[(q + EA) % kER]);
+        if (q + GA >= 0) gather_x(q + GA, W[(q + GA + kER) % kER], XG[(q + GA + kER) % kXR]);
+    }
+    __syncthreads();
+    const int32_t nbu = (nb + kER - 1) / kER * kER;   // whole groups (no early exit)
+    for (int32_t p = 0; p < nbu; p += kER) {
+#pragma unroll
+        for (int u = 0; u < kER; ++u) {
+            if (p + u + EA >= cw + 64) advance_cs_window();
+            load_entries(p + u + EA, W[(u + EA) % kER], V[(u + EA) % kER]);
+            gather_x(p + u + GA, W[(u + GA) % kER], XG[(u + GA) % kXR]);
+            if (ABL & 2) {
+#pragma unroll
+                for (int k = 0; k < CAP; ++k) asm volatile("" ::"v"(W[u][k]), "v"(V[u][k]), "v"(XG[u % kXR][k]));
+            } else {
+                apply_band(XG[u % kXR], W[u], V[u]);
+            }
+            __syncthreads();
+        }
+    }
+
+    if (n_slabs == 1 || (ABL & 4)) {
+        const int32_t nv = y_vec ? (nr & ~3) : 0;
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int32_t i = 4 * (tid + q * THREADS);
+            if (i < nv) *reinterpret_cast<float4 *>(y + r0 + i) = *reinterpret_cast<const float4 *>(&yacc[i]);
+        }
+        for (int32_t i = nv + tid; i < nr; i += THREADS) y[r0 + i] = yacc[i];
+        return;
+    }
+    // Slab hand-off (as above): publish write-through, ticket, the last tile adds
+    // y and the partials in slab order with sc1 loads.
+    const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
+    float *outp = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * ps + r0;
+    const int32_t nr4 = y_vec ? (nr & ~3) : 0;
+    const int32_t no4 = (slab != 0 || y_vec) ? (nr & ~3) : 0;
+    const __amdgpu_buffer_rsrc_t o_src = rsrc(outp, (uint64_t)nr * 4);
+    for (int32_t i = 4 * tid; i < no4; i += 4 * THREADS) {
+        const float4 v = *reinterpret_cast<const float4 *>(&yacc[i]);
+        const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                         __float_as_uint(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(u, o_src, 4u * i, 0, kAuxSc1);
+    }
+    for (int32_t i = no4 + tid; i < nr; i += THREADS)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yacc[i]), o_src, 4u * i, 0, kAuxSc1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        s_ticket = __hip_atomic_fetch_add(tickets + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_ticket != n_slabs - 1) return;
+    const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
+    float4 acc[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(y_src, 16u * (uint32_t)(tid + q * THREADS), 0, kAuxSc1);
+        acc[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                             __uint_as_float(u.w));
+    }
+    constexpr int kG = kQ >= 8 ? 2 : 4;
+    for (int32_t s0 = 1; s0 < n_slabs; s0 += kG) {
+        u32x4 pv[kG][kQ];
+#pragma unroll
+        for (int j = 0; j < kG; ++j) {
+            const int32_t sl = min(s0 + j, n_slabs - 1);
+            const __amdgpu_buffer_rsrc_t p_src =
+                rsrc(partials + (int64_t)(sl - 1) * ps + r0, (uint64_t)nr * 4);
+#pragma unroll
+            for (int q = 0; q < kQ; ++q)
+                pv[j][q] = __builtin_amdgcn_raw_buffer_load_b128(p_src, 16u * (uint32_t)(tid + q * THREADS), 0, kAuxSc1);
+        }
+#pragma unroll
+        for (int j = 0; j < kG; ++j) {
+            if (s0 + j >= n_slabs) break;
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                acc[q].x = __fadd_rn(acc[q].x, __uint_as_float(pv[j][q].x));
+                acc[q].y = __fadd_rn(acc[q].y, __uint_as_float(pv[j][q].y));
+                acc[q].z = __fadd_rn(acc[q].z, __uint_as_float(pv[j][q].z));
+                acc[q].w = __fadd_rn(acc[q].w, __uint_as_float(pv[j][q].w));
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        const int32_t i = 4 * (tid + q * THREADS);
+        if (i < nr4) *reinterpret_cast<float4 *>(y + r0 + i) = acc[q];
+    }
+    for (int32_t i = nr4 + tid; i < nr; i += THREADS) {
+        float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(y_src, 4u * i, 0, kAuxSc1));
+        for (int32_t sl = 1; sl < n_slabs; ++sl) {
+            const __amdgpu_buffer_rsrc_t p_src =
+                rsrc(partials + (int64_t)(sl - 1) * ps + r0, (uint64_t)nr * 4);
+            a = __fadd_rn(a, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(p_src, 4u * i, 0, kAuxSc1)));
+        }
+        y[r0 + i] = a;
+    }
+    if (tid == 0) __hip_atomic_store(tickets + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// SM_XBAND_GLOOK = "EA,GA" picks the lookaheads (development A/B; default 5,2).
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP>
+hipError_t launch_gtiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                         float *y, float alpha, float beta, hipStream_t s) {
+    static const int look = [] {
+        const char *e = getenv("SM_XBAND_GLOOK");
+        if (!e) return 52;
+        const int ea = atoi(e), ga = strchr(e, ',') ? atoi(strchr(e, ',') + 1) : 0;
+        return 10 * ea + ga;
+    }();
+    static const int abl = [] {
+        const char *e = getenv("SM_GBAND_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    if (abl) {
+        switch (abl) {
+#define SM_GBA(A)                                                                                  \
+    case A:                                                                                        \
+        hipLaunchKernelGGL((spmv_gband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, 5, 2, A>),       \
+                           dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s, \
+                           n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands, \
+                           xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
+                           alpha, beta);                                                           \
+        return hipGetLastError();
+        SM_GBA(1) SM_GBA(2) SM_GBA(3) SM_GBA(4) SM_GBA(7)
+#undef SM_GBA
+        default: return hipErrorInvalidValue;
+        }
+    }
+#define SM_GBL(EA, GA)                                                                            \
+    hipLaunchKernelGGL((spmv_gband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, EA, GA>),           \
+                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
+                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
+                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
+                       alpha, beta)
+    switch (look) {
+    case 32: SM_GBL(3, 2); break;
+    case 62: SM_GBL(6, 2); break;
+    case 63: SM_GBL(6, 3); break;
+    case 73: SM_GBL(7, 3); break;
+    default: SM_GBL(5, 2); break;
+    }
+#undef SM_GBL
+    return hipGetLastError();
+}
+
+template <int THREADS, int BAND_LOG2, int ROWS_LOG2>
+hipError_t launch_gkind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                        float *y, float alpha, float beta, hipStream_t s) {
+    const int64_t cap = (xb.max_chunks_per_band + THREADS / 64 - 1) / (THREADS / 64);
+#define SM_GBT(C) launch_gtiles<THREADS, BAND_LOG2, ROWS_LOG2, C>(xb, n_rows, n_cols, x, y, alpha, beta, s)
+    if (cap <= 1) return SM_GBT(1);
+    if (cap <= 2) return SM_GBT(2);
+    if (cap <= 3) return SM_GBT(3);
+    if (cap <= 4) return SM_GBT(4);
+    if (cap <= kXbMaxCap) return SM_GBT(5);
+#undef SM_GBT
+    return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
@@ -762,6 +1117,9 @@ hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     else if (xb.kind == kXbBlocked && xb.band_cols == 1 << kXbBlockedBandLog2 &&
              xb.block_rows <= 1 << kXbBlockedRowsLog2)
         e = launch_kind<kXbThreads, kXbBlockedBandLog2, kXbBlockedRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
+    else if (xb.kind == kXbGather && xb.band_cols == 1 << kXbGatherBandLog2 &&
+             xb.block_rows <= 1 << kXbGatherRowsLog2)
+        e = launch_gkind<kXbThreads, kXbGatherBandLog2, kXbGatherRowsLog2>(xb, n_rows, n_cols, x, y, alpha, beta, s);
     return e;
 }
 

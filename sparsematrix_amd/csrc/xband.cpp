@@ -34,17 +34,21 @@ namespace smamd {
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
                               int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
-                              int waves, XbandHost &out);
+                              int waves, bool col_order, XbandHost &out);
 
 // Largest block height (<= 2^bits.row, >= 64) whose bands fit the kernel's
 // register capacity (kXbMaxCap chunks per wave per band).
 bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, XbBits bits, int waves, XbandHost &out) {
+                 int64_t n_cols, XbBits bits, int waves, XbandHost &out, bool col_order,
+                 int32_t start_rows) {
     if (bits.col < 8 || bits.row < 6 || bits.rank < 2 || bits.col + bits.rank + bits.row != 32)
         return false;
-    for (int32_t br = 1 << bits.row; br >= 64; br /= 2) {
+    int32_t br0 = 1 << bits.row;
+    while (start_rows > 0 && br0 > start_rows && br0 > 64) br0 /= 2;
+    for (int32_t br = br0; br >= 64; br /= 2) {
         out.too_dense = false;
-        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, bits, waves, out)) return true;
+        if (xband_build_fixed(rp, col, val, n_rows, n_cols, br, bits, waves, col_order, out))
+            return true;
         if (!out.too_dense) return false;   // not a capacity problem: halving will not help
     }
     return false;
@@ -52,7 +56,7 @@ bool xband_build(const int32_t *rp, const int32_t *col, const float *val, int64_
 
 static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float *val,
                               int64_t n_rows, int64_t n_cols, int32_t block_rows, XbBits bits,
-                              int waves, XbandHost &out) {
+                              int waves, bool col_order, XbandHost &out) {
     out = XbandHost();
     if (n_rows <= 0 || n_cols <= 0) return false;
     const int32_t band_cols = 1 << bits.col;
@@ -98,11 +102,27 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
             if (cur[r - r0] != rp[r + 1]) return false;
         return true;
     };
+    // The gather kind lists a band's segments by first column (ties: by row), so
+    // the consecutive entries of a chunk -- one wave-instruction of x gathers --
+    // cover a narrow column window.
+    struct Seg4 { int32_t p, rl, s, e; };
+    auto walk_ordered = [&](int64_t b, auto &&emit_seg) {
+        if (!col_order) return walk(b, emit_seg);
+        std::vector<Seg4> all;
+        const bool ok = walk(b, [&](int64_t p, int32_t rl, int32_t s, int32_t e) {
+            all.push_back(Seg4{(int32_t)p, rl, s, e});
+        });
+        std::stable_sort(all.begin(), all.end(), [&](const Seg4 &a, const Seg4 &c) {
+            return a.p != c.p ? a.p < c.p : col[a.s] < col[c.s];
+        });
+        for (const Seg4 &g : all) emit_seg((int64_t)g.p, g.rl, g.s, g.e);
+        return ok;
+    };
 
     for_blocks([&](int64_t b) {
         std::vector<int32_t> fill((size_t)nb, 0);   // entries used in the open chunk
         int64_t *cnt = &chunks_of[(size_t)(b * nb)];
-        const bool ok = walk(b, [&](int64_t p, int32_t, int32_t s, int32_t e) {
+        const bool ok = walk_ordered(b, [&](int64_t p, int32_t, int32_t s, int32_t e) {
             const int32_t len = e - s;
             if (len >= bits.max_seg()) { bad[b] = 1; return; }
             if (fill[p] == 0 || fill[p] + len > 64) { cnt[p]++; fill[p] = 0; }
@@ -169,7 +189,7 @@ static bool xband_build_fixed(const int32_t *rp, const int32_t *col, const float
         std::vector<int32_t> fill((size_t)nb, 0);
         std::vector<std::vector<Seg>> open((size_t)nb);
         for (int64_t p = 0; p < nb; p++) chunk[p] = out.chunk_start[(size_t)(b * nb + p)] - 1;
-        walk(b, [&](int64_t p, int32_t rl, int32_t s, int32_t e) {
+        walk_ordered(b, [&](int64_t p, int32_t rl, int32_t s, int32_t e) {
             const int32_t len = e - s;
             if (chunk[p] < out.chunk_start[(size_t)(b * nb + p)] || fill[p] + len > 64) {
                 if (!open[p].empty()) emit_chunk(p, chunk[p], open[p]);

@@ -25,9 +25,13 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  blocked -- 16384-row blocks, 8192-column bands, columns split in slabs so each
 //             workgroup stages 4x less x; slab partial sums are combined in slab
 //             order (within the Σ|terms| tolerance, bit-identical with one slab).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2 };
+//  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
+//             column order so the x gathers of one wave-instruction hit a few cache
+//             lines; LDS holds only the accumulators (measured slower, kept for A/B).
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
+constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
 constexpr int kXbThreads = 1024;               // one workgroup per CU
 constexpr int kXbMaxBands = 4096;              // n_cols <= 32 M (blocked) / 64 M (exact)
 constexpr int kXbMaxCap = 5;                   // chunks per wave per band held in registers
@@ -47,9 +51,12 @@ struct XbandHost {
 
 // Returns false when the matrix does not fit the layout (a row segment longer
 // than bits.max_seg()-1 inside one band, unsorted columns, bands too dense even
-// for 64-row blocks, or size limits).  The block height starts at 2^bits.row and
-// halves while a band overflows the kernel's register capacity.
+// for 64-row blocks, or size limits).  The block height starts at 2^bits.row (or
+// `start_rows` when smaller and > 0) and halves while a band overflows the
+// kernel's register capacity.  col_order: a band's segments are listed by their
+// first column instead of by row (the gather kind).
 bool xband_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, XbBits bits, int waves, XbandHost &out);
+                 int64_t n_cols, XbBits bits, int waves, XbandHost &out, bool col_order = false,
+                 int32_t start_rows = 0);
 
 }  // namespace smamd

@@ -450,7 +450,7 @@ def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
 @pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 300001, 16), (9000, 70001, 40),
                                                    (70000, 1000003, 16), (5000, 1000, 5),
                                                    (40000, 20000, 3)])
-@pytest.mark.parametrize("kind,code", [("blocked", 2)])
+@pytest.mark.parametrize("kind,code", [("blocked", 2), ("gather", 3)])
 def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row, kind, code):
     """Blocked band layout (16K-row blocks, column slabs): within the Σ|terms| bound
     of the reference order; bit-identical when the matrix is a single slab; the
@@ -477,7 +477,7 @@ def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row, kind, code):
             assert_terms_close(got, want, absum)
 
 
-@pytest.mark.parametrize("kind", ["exact", "blocked"])
+@pytest.mark.parametrize("kind", ["exact", "blocked", "gather"])
 def test_xband_special_values(sm, kind):
     """Inf/NaN in x and in the stored values propagate exactly as in the reference; the
     dummy lanes (column 0, value 0) that see x[0] = inf compute NaN but never land."""
@@ -488,7 +488,7 @@ def test_xband_special_values(sm, kind):
     va[5::1009] = np.nan
     M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
         "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
-    assert M.info()["has_xband"] in (1, 2)
+    assert M.info()["has_xband"] == {"exact": 1, "blocked": 2, "gather": 3}[kind]
     rng = np.random.default_rng(8)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     x[0] = np.inf                      # what every dummy lane reads
@@ -510,7 +510,8 @@ def test_xband_special_values(sm, kind):
             assert_terms_close(got[fin], want[fin], absum[fin])
 
 
-def test_xband_blocked_signed_zeros(sm):
+@pytest.mark.parametrize("kind,code", [("blocked", 2), ("gather", 3)])
+def test_xband_blocked_signed_zeros(sm, kind, code):
     """Blocked layout: a row whose terms are all -0.0 and whose y is -0.0 stays -0.0
     across slabs (slab partials start from -0.0, the exact identity of fp32 addition);
     rows without terms in a slab keep beta*y bit-for-bit."""
@@ -518,9 +519,9 @@ def test_xband_blocked_signed_zeros(sm):
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=79)
     va = va.copy()
     va[6 * 100:6 * 200] = -0.0
-    M = _with_env("SM_XBAND_KIND", "blocked", lambda: _with_env(
+    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
         "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
-    assert M.info()["has_xband"] == 2 and M.info()["xband_slabs"] > 1, M.info()
+    assert M.info()["has_xband"] == code and M.info()["xband_slabs"] > 1, M.info()
     rng = np.random.default_rng(10)
     x = rng.uniform(0.25, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)

@@ -167,6 +167,23 @@ int main() {
         ms = timeit([&] { hipLaunchKernelGGL(lds_rmw_kernel<4096>, dim3(256), dim3(1024), 0, 0, didx, ng / 4, out); }, 10);
         printf("LDS atomicAdd f32 (16 KiB acc): %.3f ms (%.2f Gop/s)\n", ms, ng / ms / 1e6);
     }
+    // windowed gathers: each wave-instruction's 64 addresses fall in one random W-byte window
+    // of a T-byte table (column-sorted entries of a band: ~8 entries per 128-byte line at W = 1 KiB)
+    for (size_t T : {(size_t)1 << 20, (size_t)4 << 20}) {
+        for (size_t W : {(size_t)512, (size_t)1024, (size_t)2048, (size_t)4096}) {
+            const size_t te = T / 4, we = W / 4;
+            srand(2);
+            // gather_kernel: wave-instruction j of wave block b reads idx[4*(64*b + l) + j], l < 64
+            for (size_t b = 0; b < ng / 256; b++)
+                for (int j = 0; j < 4; j++) {
+                    const size_t base = ((size_t)rand() * 2654435761u) % (te - we);
+                    for (int l = 0; l < 64; l++) hidx[4 * (64 * b + l) + j] = (int)(base + (size_t)rand() % we);
+                }
+            CK(hipMemcpy(didx, hidx.data(), ng * 4, hipMemcpyHostToDevice));
+            ms = timeit([&] { hipLaunchKernelGGL(gather16_kernel, dim3(grid), dim3(256), 0, 0, didx, ng / 4, tab, out); }, 10);
+            printf("windowed gather table %5zu KiB window %5zu B: %.3f ms (%.2f Ggather/s)\n", T >> 10, W, ms, ng / ms / 1e6);
+        }
+    }
     // sequential "gather" (idx[i] = i) for reference
     for (size_t i = 0; i < ng; i++) hidx[i] = (int)i;
     CK(hipMemcpy(didx, hidx.data(), ng * 4, hipMemcpyHostToDevice));
