@@ -10,7 +10,9 @@ To measure HBM rather than the 256 MiB Infinity Cache, steps rotate over
 
 N>1 (torchrun, one process per GPU): weak scaling -- every rank owns 2^20 rows
 of a (N*2^20) x (N*2^20) matrix with global columns; a step is one RCCL
-all-gather of x (xGMI) followed by the local SpMV.  `value` is the sum of all
+all-gather of x (xGMI) and the local SpMV.  Steps are independent products
+(rotating replicas), so the all-gather of step k+1 runs beside the SpMV of step
+k (--no-overlap: strictly one after the other).  `value` is the sum of all
 ranks' algorithmic bytes divided by the max-over-ranks step time.
 
 Algorithmic bytes per SpMV: 8*nnz + 4*(rows+1) + 4*cols + 8*rows.
@@ -96,6 +98,12 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="N=1: launch each timed step from Python instead of replaying the K "
                          "steps as one captured HIP graph")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="development: one process builds rank 0's slice of a W-rank job "
+                         "(R rows x R*W columns, x filled locally instead of all-gathered)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: all-gather then SpMV per step, instead of the all-gather of "
+                         "step k+1 in flight beside the SpMV of step k")
     args = ap.parse_args()
 
     import torch
@@ -103,6 +111,7 @@ def main():
 
     import sparsematrix_amd as smd
     from sparsematrix_amd import synth
+    from sparsematrix_amd.distributed import allgather_spmv_pipelined
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -116,7 +125,8 @@ def main():
     smd.load()
 
     R = args.rows_per_rank
-    C = R * world                          # global columns (= global rows)
+    emu = args.emulate_world if world == 1 and args.emulate_world > 1 else 1
+    C = R * world * emu                    # global columns (= global rows)
     per = args.per_row
     reps = []
     for k in range(args.replicas):
@@ -125,7 +135,8 @@ def main():
         M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=local_rank)
         g = torch.Generator(device=dev).manual_seed(seed + 1)
         x_local = torch.rand(R, generator=g, device=dev) * 2 - 1
-        x_full = torch.empty(C, device=dev) if world > 1 else x_local
+        x_full = (torch.empty(C, device=dev) if world > 1 else
+                  torch.rand(C, generator=g, device=dev) * 2 - 1 if emu > 1 else x_local)
         y = torch.rand(R, generator=g, device=dev) * 2 - 1
         reps.append(dict(M=M, rp=rp, ci=ci, va=va, x_local=x_local, x_full=x_full, y=y))
         if k:
@@ -144,8 +155,28 @@ def main():
         if ev is not None:
             ev[1].record()
 
-    for i in range(args.warmup):
-        step(i)
+    # N > 1, default: steps are independent products (rotating replicas), so the
+    # all-gather of step k+1 runs beside the SpMV of step k (distributed.py,
+    # allgather_spmv_pipelined) -- still one all-gather per step, no other collective.
+    overlap = world > 1 and not args.no_overlap
+
+    def products(start, count, evs=None):
+        for j in range(count):
+            r = reps[(start + j) % len(reps)]
+
+            def local(xf, yl, r=r, e=(evs[j] if evs is not None else None)):
+                if e is not None:
+                    e[0].record()
+                r["M"].spmv(xf, yl, 1.0, 0.5, algo=args.algo)
+                if e is not None:
+                    e[1].record()
+            yield (local, r["x_local"], r["x_full"], r["y"])
+
+    if overlap:
+        allgather_spmv_pipelined(products(0, args.warmup))
+    else:
+        for i in range(args.warmup):
+            step(i)
     torch.cuda.synchronize()
     # N = 1: the K timed SpMVs are captured once into a HIP graph (capturing runs
     # nothing) and replayed as one launch, so the timed region holds the kernels
@@ -174,8 +205,11 @@ def main():
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.steps)]
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            step(args.warmup + i, events[i])
+        if overlap:
+            allgather_spmv_pipelined(products(args.warmup, args.steps, events))
+        else:
+            for i in range(args.steps):
+                step(args.warmup + i, events[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -278,8 +312,10 @@ def main():
             "config": {"workload": workload, "rows_per_rank": R, "cols": C, "nnz_per_rank": nnz,
                        "per_row": per, "replicas": args.replicas, "algo": args.algo,
                        "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
-                       "parallelism": f"row-partition x{world}" + (", RCCL all-gather(x)"
-                                                                   if world > 1 else "")},
+                       "parallelism": f"row-partition x{world}" + (
+                           ", RCCL all-gather(x)" + (" of step k+1 overlapped with SpMV k"
+                                                     if overlap else "") if world > 1 else ""),
+                       **({"emulate_world": emu} if emu > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu, "spmm": spmm,
         }
         print(json.dumps(line), flush=True)

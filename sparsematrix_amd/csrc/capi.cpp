@@ -126,11 +126,17 @@ int32_t tile_nnz_setting() {
 // (~22 TB/s chip-wide) while 4-byte gathers run at 75-200 G/s by the size of x,
 // so the sweep wins while its bytes stay under ~20x the matrix's 8 B per term.
 // SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
-XbKind xband_kind_setting() {
+// SM_XBAND_KIND=blocked|gather forces a kind.  Otherwise: blocked, or gather for
+// very wide matrices -- measured per rank of the bench's row partition (1M rows,
+// 16 terms per row): 2M columns 61 vs 65 us, 4M 83 vs 85 us, 8M 145
+// vs 121 us (blocked vs gather).  Past ~5M columns each blocked tile sweeps more x
+// through LDS (8 MiB at 8M) than gathering its terms' x values costs.
+XbKind xband_kind_setting(const sm_matrix *m) {
     const char *e = getenv("SM_XBAND_KIND");
     if (e && strcmp(e, "exact") == 0) return kXbExact;
     if (e && strcmp(e, "gather") == 0) return kXbGather;
-    return kXbBlocked;
+    if (e && strcmp(e, "blocked") == 0) return kXbBlocked;
+    return m->n_cols > 5 * ((int64_t)1 << 20) ? kXbGather : kXbBlocked;
 }
 
 bool want_xband(const sm_matrix *m) {
@@ -138,7 +144,7 @@ bool want_xband(const sm_matrix *m) {
     if (e && atoi(e) == 0) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
     if (e && atoi(e) == 1) return true;
-    const XbKind kind = xband_kind_setting();
+    const XbKind kind = xband_kind_setting(m);
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
                           : kind == kXbGather ? kXbGatherRowsLog2
                                               : kXbBlockedRowsLog2;
@@ -321,7 +327,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
         SM_TRY_HIP(hipMemcpy(m->d_val, val, (size_t)m->nnz * 4, hipMemcpyHostToDevice));
     }
     sm_status st2 = upload_plan(m, rp);
-    if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting());
+    if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting(m));
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     return st2;
 }
@@ -531,7 +537,7 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
                 e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
         }
         st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR for band layout / relabeling");
-        if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting());
+        if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting(m.get()));
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }

@@ -43,3 +43,32 @@ def allgather_spmv(local_spmv: Callable, x_local, x_full, y_local, group=None):
     import torch.distributed as dist
     dist.all_gather_into_tensor(x_full, x_local, group=group)
     return local_spmv(x_full, y_local)
+
+
+def allgather_spmv_pipelined(products, group=None):
+    """A sequence of independent products, each `(local_spmv, x_local, x_full,
+    y_local)`: the all-gather of product k+1 is in flight while product k's SpMV
+    runs -- still one all-gather per product and no other collective.
+
+    Ordering (GPU ranks, RCCL): the all-gather of k+1 is issued after the wait on
+    all-gather k and before SpMV k is enqueued, so RCCL's stream waits for what the
+    compute stream holds at that point (SpMV k-1) and then runs beside SpMV k;
+    x_full of k+1 may therefore be the buffer SpMV k-1 read, never one still
+    being read.  On gloo (CPU) the waits are blocking and the order is the plain
+    one.  Returns the number of products."""
+    import torch.distributed as dist
+    it = iter(products)
+    nxt = next(it, None)
+    if nxt is None:
+        return 0
+    work = dist.all_gather_into_tensor(nxt[2], nxt[1], group=group, async_op=True)
+    n = 0
+    while nxt is not None:
+        cur, cur_work = nxt, work
+        cur_work.wait()
+        nxt = next(it, None)
+        if nxt is not None:
+            work = dist.all_gather_into_tensor(nxt[2], nxt[1], group=group, async_op=True)
+        cur[0](cur[2], cur[3])
+        n += 1
+    return n

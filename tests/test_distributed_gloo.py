@@ -88,3 +88,58 @@ def test_partition_bounds():
         assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
         assert max(e - s for s, e in b) - min(e - s for s, e in b) <= 1
         assert p.equal() == (n % w == 0)
+
+
+def _worker_pipelined(rank, world, port, n, n_prod, out_q):
+    from sparsematrix_amd.distributed import allgather_spmv_pipelined
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rp, ci, va, _, y = _problem(n, 16, seed=9)
+    part = RowPartition(n, world)
+    r0, r1 = part.bounds(rank)
+    lrp, lci, lva = slice_csr(rp, ci, va, r0, r1)
+    xs = [np.random.default_rng(100 + k).uniform(-1, 1, n).astype(np.float32)
+          for k in range(n_prod)]
+    # two x_full buffers rotated as in bench.py: product k+1 gathers into the one product k-1 read
+    bufs = [torch.empty(n, dtype=torch.float32) for _ in range(2)]
+    outs = [None] * n_prod
+
+    def product(k):
+        def local(xf, yl):
+            assert np.array_equal(xf.numpy(), xs[k])
+            outs[k] = oracle.csr_spmv(lrp, lci, lva, xf.numpy(), yl, 1.0, 0.5)
+        return (local, torch.from_numpy(xs[k][r0:r1].copy()), bufs[k % 2], y[r0:r1].copy())
+
+    assert allgather_spmv_pipelined(product(k) for k in range(n_prod)) == n_prod
+    res = []
+    for k in range(n_prod):
+        gathered = [torch.empty(r1 - r0, dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(outs[k]))
+        res.append(np.concatenate([g.numpy() for g in gathered]))
+    if rank == 0:
+        out_q.put(np.stack(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_pipelined_allgather_matches_single_process():
+    """Independent products with the all-gather of k+1 issued before SpMV k:
+    every product equals the single-process oracle bit-for-bit."""
+    oracle.build()
+    world, n, n_prod = 2, 4000, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, n, n_prod, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rp, ci, va, _, y = _problem(n, 16, seed=9)
+    for k in range(n_prod):
+        x = np.random.default_rng(100 + k).uniform(-1, 1, n).astype(np.float32)
+        want = oracle.csr_spmv(rp, ci, va, x, y, 1.0, 0.5)
+        assert np.array_equal(got[k].view(np.uint32), want.view(np.uint32)), k
