@@ -259,7 +259,16 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
 
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
-    const int32_t tile = tile_nnz_setting();
+    int32_t tile = tile_nnz_setting();
+    // Power-law rows (longest row > 64x the mean, e.g. R-MAT): 2048-term tiles
+    // balance the workgroups better -- R-MAT scale 24: 2.34 ms vs 2.43 ms at 4096
+    // (profiles/r01_rmat24_sweep.txt).  SM_TILE_NNZ overrides.
+    if (!getenv("SM_TILE_NNZ") && m->n_rows > 0) {
+        int64_t longest = 0;
+        for (int64_t r = 0; r < m->n_rows; r++)
+            longest = std::max<int64_t>(longest, (int64_t)rp_host[r + 1] - rp_host[r]);
+        if ((double)longest > 64.0 * (double)m->nnz / (double)m->n_rows) tile = 2048;
+    }
     plan_rows(rp_host, m->n_rows, tile, kTileRows, kLongChunk, kSerialRowMax, ph);
     std::vector<Tile> tiles(ph.tiles.size());
     for (size_t i = 0; i < tiles.size(); i++)
