@@ -19,6 +19,8 @@ def main() -> None:
     ap.add_argument("--per-row", type=int, default=16)
     ap.add_argument("--n", default="32")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ab-env", default="SM_SPMM_OLD",
+                    help="variable toggled 1 (\"old\") / 0 (\"new\"), e.g. SM_SPMM_NT")
     args = ap.parse_args()
 
     import numpy as np
@@ -40,7 +42,7 @@ def main() -> None:
         Y0 = torch.rand((R, N), generator=g, device=dev) * 2 - 1
         res = {}
         for old in ("1", "0"):
-            os.environ["SM_SPMM_OLD"] = old
+            os.environ[args.ab_env] = old
             Y = Y0.clone()
             for _ in range(3):
                 M.spmm(X, Y, 1.0, 0.5)
@@ -57,13 +59,13 @@ def main() -> None:
             M.spmm(X, Y, 1.0, 0.5)
             res[old] = (ms, Y.cpu().numpy().view(np.uint32))
         same = bool(np.array_equal(res["0"][1], res["1"][1]))
-        line = {"n_rhs": N, "old_ms": round(res["1"][0], 4), "new_ms": round(res["0"][0], 4),
+        line = {"ab_env": args.ab_env, "n_rhs": N, "old_ms": round(res["1"][0], 4), "new_ms": round(res["0"][0], 4),
                 "gflops_new": round(2.0 * nnz * N / (res["0"][0] * 1e-3) / 1e9, 1),
                 "bit_identical": same}
         print(json.dumps(line), flush=True)
         out.append(line)
         del X, Y0, Y
-    os.environ.pop("SM_SPMM_OLD", None)
+    os.environ.pop(args.ab_env, None)
 
 
 if __name__ == "__main__":
