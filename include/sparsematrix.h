@@ -122,6 +122,17 @@ SM_API sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, 
                                             int32_t table_size, sm_trans trans,
                                             int32_t device, sm_matrix **out);
 
+/* Same as sm_create_from_dense_index with the index already on `device`
+ * (`d_index`, rows x stride bytes; `table` stays a host pointer): the scan runs
+ * on the device (count, host prefix sum, fill) and yields
+ * the same CSR bit for bit.  No reference stream is kept, so sm_copy_ref_stream
+ * does not apply.  Synchronises `stream`. */
+SM_API sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows,
+                                                   int32_t cols, int32_t stride,
+                                                   const float *table, int32_t table_size,
+                                                   sm_trans trans, int32_t device,
+                                                   sm_stream stream, sm_matrix **out);
+
 /* Additive CSR ingestion (no reference equivalent: the reference cannot encode
  * the north-star sizes).  B is n_rows x n_cols; row_ptr has
  * n_rows+1 entries.  Host pointers, validated on the host. */

@@ -35,7 +35,8 @@ ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4}
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
     "sm_version", "sm_status_string", "sm_last_error", "sm_device_count",
-    "sm_create_from_dense_index", "sm_create_from_csr", "sm_create_from_csr_device",
+    "sm_create_from_dense_index", "sm_create_from_dense_index_device", "sm_create_from_csr",
+    "sm_create_from_csr_device",
     "sm_destroy", "sm_get_info", "sm_num_rows", "sm_num_cols", "sm_copy_ref_stream",
     "sm_copy_csr", "sm_to_dense", "sm_equal", "sm_spmv", "sm_spmm", "sm_addmatmat",
     "sm_addmatmat_host", "sm_beta_scale", "sm_transpose", "sm_panel_kernel", "sm_stream_sync",
@@ -74,6 +75,8 @@ def _declare(L):
         "sm_device_count": ([C.POINTER(_i32)], C.c_int),
         "sm_create_from_dense_index": ([_vp, _i32, _i32, _i32, _vp, _i32, C.c_int, _i32,
                                         C.POINTER(_vp)], C.c_int),
+        "sm_create_from_dense_index_device": ([_vp, _i32, _i32, _i32, _vp, _i32, C.c_int, _i32,
+                                               _vp, C.POINTER(_vp)], C.c_int),
         "sm_create_from_csr": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, C.POINTER(_vp)], C.c_int),
         "sm_create_from_csr_device": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp,
                                        C.POINTER(_vp)], C.c_int),

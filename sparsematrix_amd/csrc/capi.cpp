@@ -445,6 +445,98 @@ sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t
     return SM_OK;
 }
 
+// CopyForm's scan on the device (encode_dev.hip): count, host prefix sum, fill, then the
+// device-CSR constructor (validation, plans, band layout).  Same CSR as the host
+// encoder, bit for bit; no reference stream is kept (like a CSR-built matrix).
+sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows, int32_t cols,
+                                            int32_t stride, const float *table,
+                                            int32_t table_size, sm_trans trans, int32_t device,
+                                            sm_stream stream, sm_matrix **out) {
+    if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
+    *out = nullptr;
+    if (table_size < 0 || table_size > 255)
+        return fail(SM_ERR_INVALID_ARG, "table_size %d not in [0, 255]", table_size);
+    if (rows < 0 || cols < 0 || stride < cols)
+        return fail(SM_ERR_INVALID_ARG, "bad shape rows=%d cols=%d stride=%d", rows, cols, stride);
+    if (trans != SM_NO_TRANS && trans != SM_TRANS) return fail(SM_ERR_INVALID_ARG, "bad trans");
+    if (table_size == 0 || rows == 0 || cols == 0)   // nothing to scan: the host rules apply
+        return sm_create_from_dense_index(nullptr, rows, cols, stride, table, table_size, trans,
+                                          device, out);
+    if (!d_index || !table) return fail(SM_ERR_INVALID_ARG, "null index/table");
+    sm_status st = check_device(device);
+    if (st != SM_OK) return st;
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    hipStream_t s = (hipStream_t)stream;
+    const bool tr = trans == SM_TRANS;
+    const uint8_t T = (uint8_t)table_size;
+    const int64_t nb = tr ? rows : cols;    // rows of B = columns of S
+    const int64_t kb = tr ? cols : rows;    // columns of B = rows of S
+    // NoTrans: index rows split in chunks so the count/fill grids fill the chip.
+    const int32_t chunk_rows = tr ? rows : std::max<int32_t>(256, (rows + 63) / 64);
+    const int32_t n_chunks = tr ? 1 : (rows + chunk_rows - 1) / chunk_rows;
+    const int64_t n_cnt = tr ? nb : (int64_t)n_chunks * nb;
+    std::vector<int32_t> cnt((size_t)n_cnt);
+    int32_t *d_cnt = nullptr, *d_offs = nullptr, *d_rp = nullptr, *d_col = nullptr;
+    float *d_table = nullptr, *d_val = nullptr;
+    int64_t scratch = 0;
+    auto cleanup = [&]() {
+        (void)hipFree(d_cnt); (void)hipFree(d_offs); (void)hipFree(d_rp);
+        (void)hipFree(d_col); (void)hipFree(d_val); (void)hipFree(d_table);
+    };
+    hipError_t e = dev_alloc(&d_cnt, n_cnt, scratch);
+    if (e == hipSuccess)
+        e = launch_encode_count(d_index, rows, cols, stride, tr, chunk_rows, n_chunks, T, d_cnt, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(cnt.data(), d_cnt, (size_t)n_cnt * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { cleanup(); return hip_fail(e, "dense index count"); }
+    // Prefix sums: row_ptr over B rows; per (chunk, row) start offsets.
+    std::vector<int64_t> rp64((size_t)nb + 1, 0);
+    std::vector<int32_t> offs((size_t)n_cnt);
+    for (int64_t j = 0; j < nb; j++) {
+        int64_t t = 0;
+        for (int32_t ch = 0; ch < n_chunks; ch++) t += cnt[(size_t)(ch * nb + j)];
+        rp64[(size_t)j + 1] = rp64[(size_t)j] + t;
+    }
+    const int64_t nnz = rp64[(size_t)nb];
+    st = check_sizes(nb, kb, nnz);
+    if (st != SM_OK) { cleanup(); return st; }
+    for (int64_t j = 0; j < nb; j++) {
+        int64_t o = rp64[(size_t)j];
+        for (int32_t ch = 0; ch < n_chunks; ch++) {
+            offs[(size_t)(ch * nb + j)] = (int32_t)o;
+            o += cnt[(size_t)(ch * nb + j)];
+        }
+    }
+    std::vector<int32_t> rp32(rp64.begin(), rp64.end());
+    std::vector<float> tb(table, table + table_size);
+    tb.push_back(0.0f);
+    e = dev_alloc(&d_offs, n_cnt, scratch);
+    if (e == hipSuccess) e = dev_alloc(&d_rp, nb + 1, scratch);
+    if (e == hipSuccess) e = dev_alloc(&d_table, (int64_t)tb.size(), scratch);
+    if (e == hipSuccess) e = dev_alloc(&d_col, std::max<int64_t>(nnz, 1), scratch);
+    if (e == hipSuccess) e = dev_alloc(&d_val, std::max<int64_t>(nnz, 1), scratch);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_offs, offs.data(), (size_t)n_cnt * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_rp, rp32.data(), rp32.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_table, tb.data(), tb.size() * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = launch_encode_fill(d_index, rows, cols, stride, tr, chunk_rows, n_chunks, T,
+                               tr ? d_rp : d_offs, d_table, d_col, d_val, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);   // host vectors above go out of scope
+    if (e != hipSuccess) { cleanup(); return hip_fail(e, "dense index fill"); }
+    st = sm_create_from_csr_device(nb, kb, nnz, d_rp, d_col, d_val, device, stream, out);
+    cleanup();
+    if (st == SM_OK) {
+        (*out)->table_size = table_size;
+        (*out)->table = std::move(tb);
+    }
+    return st;
+}
+
 sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *row_ptr,
                              const int32_t *col_idx, const float *val, int32_t device,
                              sm_matrix **out) {

@@ -97,6 +97,15 @@ hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, cons
 hipError_t launch_beta(float *c, int32_t m, int32_t n, int64_t ldc, float beta, hipStream_t s);
 hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, float *sa,
                             int64_t ldsa, hipStream_t s);
+// Device CopyForm scan (encode_dev.hip).  trans: one count per index row (B row);
+// otherwise one count per (chunk of chunk_rows index rows, index column), chunk-major.
+hipError_t launch_encode_count(const uint8_t *dm, int32_t rows, int32_t cols, int32_t stride,
+                               bool trans, int32_t chunk_rows, int32_t n_chunks, uint8_t T,
+                               int32_t *cnt, hipStream_t s);
+hipError_t launch_encode_fill(const uint8_t *dm, int32_t rows, int32_t cols, int32_t stride,
+                              bool trans, int32_t chunk_rows, int32_t n_chunks, uint8_t T,
+                              const int32_t *offs, const float *table, int32_t *col, float *val,
+                              hipStream_t s);
 hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
                            const int32_t *col, int32_t *d_flag, hipStream_t s);
 // Dense decode: out is zeroed by the caller.  b_layout: out[row*stride+col]

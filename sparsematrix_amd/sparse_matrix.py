@@ -130,6 +130,32 @@ class SparseMatrix:
         self._h = h
 
     @classmethod
+    def from_dense_index(cls, index, rows: int, cols: int, stride: int, vals,
+                         val_table_size: int, trans: int = SblasNoTrans, device: int = 0,
+                         stream=None) -> "SparseMatrix":
+        """CopyForm from a uint8 id matrix (rows x stride): a torch cuda tensor is scanned
+        on the device (sm_create_from_dense_index_device), anything else on the host."""
+        self = cls(device=device)
+        if not _is_device(index):
+            self.CopyForm(index, rows, cols, stride, vals, val_table_size, trans)
+            return self
+        import torch
+        assert index.dtype == torch.uint8
+        dm = index.contiguous()
+        if dm.numel() < rows * stride and rows * cols > 0 and val_table_size > 0:
+            raise ValueError("index smaller than rows * stride")
+        tb = np.zeros(max(int(val_table_size), 1), np.float32)
+        if val_table_size:
+            tb[:val_table_size] = np.asarray(vals, np.float32).reshape(-1)[:val_table_size]
+        h = C.c_void_p()
+        st = self._L.sm_create_from_dense_index_device(_ptr(dm), rows, cols, stride, _ptr(tb),
+                                                       val_table_size, int(trans), device,
+                                                       _stream_of(dm, stream), C.byref(h))
+        check(st, "from_dense_index")
+        self._h = h
+        return self
+
+    @classmethod
     def from_csr(cls, row_ptr, col_idx, val, n_cols: int, device: int = 0,
                  stream=None) -> "SparseMatrix":
         """Additive CSR ingestion of B (n_rows x n_cols): numpy (host) or torch cuda tensors."""

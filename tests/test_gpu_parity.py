@@ -635,3 +635,47 @@ def test_relabel_bit_identical(sm, n_rows, n_cols, per_row, force):
         got = to_host(y)
         assert np.array_equal(bits(got), bits(to_host(y_ref))), algo
         assert np.array_equal(bits(got), bits(want)), algo   # rows of <= 8 terms
+
+
+# ------------------------------------------------------------- device CopyForm scan
+@pytest.mark.parametrize("name", case_names())
+def test_golden_device_encode(sm, name):
+    """CopyForm's scan on the device (sm_create_from_dense_index_device): the CSR of B
+    equals the host encoder's bit for bit, and B decodes to the reference's own
+    dense output (golden fixture)."""
+    torch = torch_dev()
+    c = load_case(name)
+    H = _from_case(sm, c)
+    dm = np.ascontiguousarray(c.dm, np.uint8).reshape(-1)
+    D = sm.SparseMatrix.from_dense_index(torch.from_numpy(dm.copy()).cuda(), c.rows, c.cols,
+                                         c.stride, c.table, c.table_size,
+                                         sm.SblasTrans if c.trans else sm.SblasNoTrans)
+    assert (D.NumRows(), D.NumCols()) == (H.NumRows(), H.NumCols())
+    for a, b in zip(H.csr(), D.csr()):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    if c.s_rows and c.s_cols:
+        got = D.CopyTo(None, c.s_rows, sm.SblasTrans)[: c.s_cols * c.s_rows]
+        assert bits_equal(got.reshape(c.s_cols, c.s_rows), c.dense_b())
+
+
+@pytest.mark.parametrize("trans", [0, 1])
+@pytest.mark.parametrize("rows,cols,stride,dens,T", [(3000, 2000, 2048, 0.01, 255),
+                                                     (700, 1300, 1333, 0.05, 200),
+                                                     (1, 7, 7, 0.5, 3), (5, 300, 300, 0.0, 255),
+                                                     (20000, 600, 640, 0.02, 17)])
+def test_device_encode_random_matches_host(sm, trans, rows, cols, stride, dens, T):
+    """Random id matrices with ids >= table_size (skipped), padding columns past `cols`,
+    empty rows/columns, a single row, and (20000 rows) many row chunks."""
+    torch = torch_dev()
+    rng = np.random.default_rng(rows + cols + trans)
+    dm = np.full((rows, stride), 255, np.uint8)
+    keep = rng.random((rows, cols)) < dens
+    dm[:, :cols] = np.where(keep, rng.integers(0, 256, (rows, cols)), 255)
+    dm[:, cols:] = rng.integers(0, 256, (rows, stride - cols))   # never read
+    table = rng.uniform(-1, 1, T).astype(np.float32)
+    H = sm.SparseMatrix(dm, rows, cols, stride, table, T, trans)
+    D = sm.SparseMatrix.from_dense_index(torch.from_numpy(dm.reshape(-1).copy()).cuda(), rows,
+                                         cols, stride, table, T, trans)
+    for a, b in zip(H.csr(), D.csr()):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert D.info()["nnz"] == H.info()["nnz"]
