@@ -839,7 +839,31 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         e = beta != 1.0f ? launch_beta(c, m, (int32_t)n, ldc, beta, s) : hipSuccess;
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat beta");
     }
-    // C^T = B A^T, read in place: X(kk, i) = a[i*lda + kk], Y(j, i) = c[i*ldc + j]
+    if (algo != SM_ALGO_PARITY && m <= 128 && k > 0) {
+        // C^T = B A^T through the row-panel SpMM (the reference transposes too,
+        // kernel.cc:31-187): X = A^T (k x mp), Y = C^T (n x mp) in a stream-ordered
+        // workspace, mp = m rounded up to 4 (the padding columns are never copied
+        // back), then C = Y^T.  Same terms in the same order as the in-place kernel
+        // below (bit-identical); the matrix is streamed once instead of m times.
+        const int64_t mp = (m + 3) & ~3;
+        float *ws = nullptr;
+        e = hipMallocAsync((void **)&ws, (size_t)(k + n) * mp * sizeof(float), s);
+        float *X = ws, *Y = ws + k * mp;
+        if (e == hipSuccess) e = launch_transpose(a, m, (int32_t)k, lda, X, mp, s);
+        if (e == hipSuccess) e = launch_transpose(c, m, (int32_t)n, ldc, Y, mp, s);
+        if (e == hipSuccess)
+            e = launch_spmm_rowpanel((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val,
+                                     (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, s);
+        if (e == hipSuccess) e = launch_transpose(Y, (int32_t)n, m, mp, c, ldc, s);
+        if (ws) {
+            const hipError_t ef = hipFreeAsync(ws, s);
+            if (e == hipSuccess) e = ef;
+        }
+        e = after_launch(e, s, "sm_addmatmat");
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat (row panels)");
+    }
+    // Parity (or m > 128): C^T = B A^T read in place, one thread per output:
+    // X(kk, i) = a[i*lda + kk], Y(j, i) = c[i*ldc + j].
     e = launch_spmm_generic((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val, a, 1, lda, c,
                             1, ldc, alpha, beta, false, s);
     e = after_launch(e, s, "sm_addmatmat");
