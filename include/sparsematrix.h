@@ -184,7 +184,9 @@ SM_API sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const f
                          sm_stream stream);
 
 /* AddMatMat (sparse-matrix.cc:139-194) on device pointers:
- * C (m x n, ldc) = alpha * A (m x k, lda) * S + beta * C. */
+ * C (m x n, ldc) = alpha * A (m x k, lda) * S + beta * C.
+ * 2 <= m <= 128 with algo != SM_ALGO_PARITY: transposes + row-panel SpMM in a
+ * per-call workspace; the call synchronises `stream` before returning. */
 SM_API sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
                               float *c, int32_t ldc, float alpha, float beta, sm_algo algo,
                               sm_stream stream);

@@ -846,8 +846,13 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         // back), then C = Y^T.  Same terms in the same order as the in-place kernel
         // below (bit-identical); the matrix is streamed once instead of m times.
         const int64_t mp = (m + 3) & ~3;
+        // Workspace per call like the reference's temp buffer (sparse-matrix.cc:155-161),
+        // freed after the stream drains (the call returns with the product done).  A
+        // stream-ordered hipMallocAsync workspace gave wrong sums when driven from the C++
+        // harness (tools/blas_test.cc, legacy null stream), so it is not used.
         float *ws = nullptr;
-        e = hipMallocAsync((void **)&ws, (size_t)(k + n) * mp * sizeof(float), s);
+        const size_t ws_bytes = (size_t)(k + n) * mp * sizeof(float);
+        e = hipMalloc((void **)&ws, ws_bytes);
         float *X = ws, *Y = ws + k * mp;
         if (e == hipSuccess) e = launch_transpose(a, m, (int32_t)k, lda, X, mp, s);
         if (e == hipSuccess) e = launch_transpose(c, m, (int32_t)n, ldc, Y, mp, s);
@@ -856,7 +861,9 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
                                      (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, s);
         if (e == hipSuccess) e = launch_transpose(Y, (int32_t)n, m, mp, c, ldc, s);
         if (ws) {
-            const hipError_t ef = hipFreeAsync(ws, s);
+            hipError_t ef = hipStreamSynchronize(s);
+            const hipError_t ef2 = hipFree(ws);
+            if (ef == hipSuccess) ef = ef2;
             if (e == hipSuccess) e = ef;
         }
         e = after_launch(e, s, "sm_addmatmat");
@@ -889,7 +896,9 @@ sm_status sm_addmatmat_host(const sm_matrix *mat, const float *a, int32_t m, int
     if (e == hipSuccess) e = hipMemcpy(dc, c, (size_t)c_elems * 4, hipMemcpyHostToDevice);
     sm_status st = SM_OK;
     if (e == hipSuccess) {
-        st = sm_addmatmat(mat, da, m, lda, dc, ldc, alpha, beta, SM_ALGO_PARITY, nullptr);
+        // Bit-exact either way: m = 1 the parity SpMV, m > 1 the row-panel path.
+        st = sm_addmatmat(mat, da, m, lda, dc, ldc, alpha, beta,
+                          m == 1 ? SM_ALGO_PARITY : SM_ALGO_AUTO, nullptr);
         if (st == SM_OK) e = hipMemcpy(c, dc, (size_t)c_elems * 4, hipMemcpyDeviceToHost);
     }
     (void)hipFree(da);
