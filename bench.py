@@ -118,10 +118,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (use torch.distributed.run)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # Development rehearsal only: SM_BENCH_DEVICE pins every rank to one GPU and
+    # SM_BENCH_BACKEND=gloo replaces RCCL, so the N>1 code path can run on a one-GPU box.
+    dev_index = int(os.environ.get("SM_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SM_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     smd.load()
 
     R = args.rows_per_rank
@@ -132,7 +139,7 @@ def main():
     for k in range(args.replicas):
         seed = 2 + 1000 * k + 7919 * rank
         rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
-        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=local_rank)
+        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index)
         g = torch.Generator(device=dev).manual_seed(seed + 1)
         x_local = torch.rand(R, generator=g, device=dev) * 2 - 1
         x_full = (torch.empty(C, device=dev) if world > 1 else
