@@ -733,6 +733,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
         case 2048: return SM_XBT(4, 2048);
         case 37: return SM_XBT(4, 37);
         case 4096: return SM_XBT(4, 4096);
+        case 8192: return SM_XBT(4, 8192);   // no ablation: the full kernel at CAP 4 (baseline for the others)
         case 4097: return SM_XBT(4, 4097);
         default: return hipErrorInvalidValue;
         }
