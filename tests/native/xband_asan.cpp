@@ -1,9 +1,11 @@
 // Host-only check of the column-band builder (sparsematrix_amd/csrc/xband.cpp),
-// built with AddressSanitizer by tests/test_xband_builder.py: for both layouts
-// (exact, blocked) and several shapes, every term appears exactly once, per row
+// built with AddressSanitizer by tests/test_xband_builder.py: for the three layouts
+// (exact, blocked, gather = blocked bits with column-ordered segments) and several
+// shapes, every term appears exactly once, per row
 // in ascending column order (bands ascend, ranks ascend inside a band), with
 // correct ranks, no row's segment split across chunks, the register capacity
-// respected, and padding decoding as dummies.
+// respected, padding decoding as dummies, and (gather) a band's chunks in ascending
+// order of their segments' first columns.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -15,7 +17,7 @@
 using namespace smamd;
 
 static int check(XbBits bits, int waves, int64_t n_rows, int64_t n_cols, int per_row,
-                 unsigned seed, bool expect_ok) {
+                 unsigned seed, bool expect_ok, bool col_order = false) {
     std::mt19937 rng(seed);
     std::vector<int32_t> rp(n_rows + 1), col;
     std::vector<float> val;
@@ -28,7 +30,8 @@ static int check(XbBits bits, int waves, int64_t n_rows, int64_t n_cols, int per
         rp[r + 1] = (int32_t)col.size();
     }
     XbandHost xh;
-    const bool ok = xband_build(rp.data(), col.data(), val.data(), n_rows, n_cols, bits, waves, xh);
+    const bool ok = xband_build(rp.data(), col.data(), val.data(), n_rows, n_cols, bits, waves, xh,
+                                col_order);
     if (ok != expect_ok) { printf("FAIL build=%d expected %d\n", ok, expect_ok); return 1; }
     if (!ok) return 0;
     if (xh.block_rows > (1 << bits.row) || xh.band_cols != (1 << bits.col)) {
@@ -42,8 +45,10 @@ static int check(XbBits bits, int waves, int64_t n_rows, int64_t n_cols, int per
             const int64_t c0 = xh.chunk_start[b * xh.n_bands + p];
             const int64_t c1 = xh.chunk_start[b * xh.n_bands + p + 1];
             std::vector<int64_t> owner(xh.block_rows, -1);   // chunk holding the row's segment
+            uint32_t prev_max = 0;                             // col_order: previous chunk's last first-column
             for (int64_t c = c0; c < c1; c++) {
                 std::vector<int> seen_rows;
+                uint32_t cmin = 0xFFFFFFFFu, cmax = 0;
                 for (int l = 0; l < 64; l++) {
                     const size_t idx = (size_t)(c * 64 + l);
                     const uint32_t w = xh.word[idx] ^ bits.dummy_word();
@@ -64,6 +69,11 @@ static int check(XbBits bits, int waves, int64_t n_rows, int64_t n_cols, int per
                         printf("FAIL rank\n"); return 1; }
                     seen_rows.push_back((int)rl);
                     got[r].push_back({(int32_t)(p * xh.band_cols + cl), xh.val[idx]});
+                    if (rank == 0) { cmin = std::min(cmin, cl); cmax = std::max(cmax, cl); }
+                }
+                if (col_order && cmin != 0xFFFFFFFFu) {
+                    if (cmin < prev_max) { printf("FAIL column order across chunks\n"); return 1; }
+                    prev_max = cmax;
                 }
             }
         }
@@ -81,16 +91,19 @@ int main() {
     const XbBits exact = xb_bits(kXbExactBandLog2, kXbExactRowsLog2);
     const XbBits blocked = xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);
     int bad = 0;
-    const struct { XbBits bits; int waves; } kinds[] = {
-        {exact, kXbThreads / 64}, {blocked, kXbComputeWaves}};
+    const XbBits gather = xb_bits(kXbGatherBandLog2, kXbGatherRowsLog2);
+    const struct { XbBits bits; int waves; bool col_order; } kinds[] = {
+        {exact, kXbThreads / 64, false}, {blocked, kXbComputeWaves, false},
+        {gather, kXbThreads / 64, true}};
     for (const auto &k : kinds) {
-        bad += check(k.bits, k.waves, 200003, 300001, 16, 1, true);
-        bad += check(k.bits, k.waves, 9000, 70001, 40, 2, true);    // dense bands: smaller blocks
-        bad += check(k.bits, k.waves, 4096, 32768, 7, 3, true);
-        bad += check(k.bits, k.waves, 5000, 1000, 5, 4, true);
-        bad += check(k.bits, k.waves, 5000, 40000, 8, 5, true);
-        bad += check(k.bits, k.waves, 70000, 1000003, 16, 7, true);
-        bad += check(k.bits, k.waves, 300, 20000, 400, 6, false);   // a row's segment too long for the rank field
+        const bool co = k.col_order;
+        bad += check(k.bits, k.waves, 200003, 300001, 16, 1, true, co);
+        bad += check(k.bits, k.waves, 9000, 70001, 40, 2, true, co);    // dense bands: smaller blocks
+        bad += check(k.bits, k.waves, 4096, 32768, 7, 3, true, co);
+        bad += check(k.bits, k.waves, 5000, 1000, 5, 4, true, co);
+        bad += check(k.bits, k.waves, 5000, 40000, 8, 5, true, co);
+        bad += check(k.bits, k.waves, 70000, 1000003, 16, 7, true, co);
+        bad += check(k.bits, k.waves, 300, 20000, 400, 6, false, co);   // a row's segment too long for the rank field
     }
     printf(bad ? "xband_asan: FAILED\n" : "xband_asan: ok\n");
     return bad ? 1 : 0;
