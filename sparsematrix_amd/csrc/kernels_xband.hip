@@ -759,10 +759,11 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
 // band p+EA, gathers the x values of band p+GA (their words arrived EA-GA
 // bands ago) and applies band p: only the accumulator read and write touch LDS,
 // no x slice is stored and LDS holds nothing but the accumulators.  One barrier
-// per band keeps a row's terms in ascending column order.  Measured slower than
-// the LDS-staged kernel on config 2 (54 vs 48 us): the gathers and
-// the apply each add ~10 us that do not overlap the entry stream; 32K-row blocks
-// (half the x per term) pay more in their 8-slab hand-off than they save.
+// per band keeps a row's terms in ascending column order.  Slower than the
+// LDS-staged kernel on config 2 (54 vs 48 us, DESIGN.md §3.4: the gathers and the
+// apply each add ~10 us that do not overlap the entry stream) but faster on wide
+// slices, where a blocked tile would sweep many MiB of x through LDS for few
+// terms: AUTO takes it past 5M columns (8M: 121 vs 145 us).
 template <int N>
 __device__ __forceinline__ void pin_one(float *a) {
 #pragma unroll
