@@ -32,6 +32,7 @@ enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
+constexpr int kXbGatherWideBandLog2 = 15;      // wide slices: 32K-column bands, 3-bit ranks
 constexpr int kXbThreads = 1024;               // one workgroup per CU
 constexpr int kXbMaxBands = 4096;              // n_cols <= 32 M (blocked) / 64 M (exact)
 constexpr int kXbMaxCap = 5;                   // chunks per wave per band held in registers
