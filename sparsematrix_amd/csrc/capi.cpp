@@ -126,19 +126,20 @@ int32_t tile_nnz_setting() {
 // (~22 TB/s chip-wide) while 4-byte gathers run at 75-200 G/s by the size of x,
 // so the sweep wins while its bytes stay under ~20x the matrix's 8 B per term.
 // SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
-// SM_XBAND_KIND=blocked|gather forces a kind.  Otherwise: blocked, or gather (with
-// 32K-column bands) for wide matrices -- measured per rank of the bench's row
-// partition (1M rows, 16 terms per row): 2M columns 61 vs 66 us, 4M 83
-// vs 74 us, 8M 145 vs 93 us (blocked vs wide gather).  Past ~3M columns each blocked
-// tile sweeps more x through LDS (4 MiB at 4M) than gathering its terms' x costs.
-constexpr int64_t kWideCols = 3 * ((int64_t)1 << 20);   // "wide": > 3M columns
+// SM_XBAND_KIND=blocked|gather forces a kind.  Otherwise: blocked, or gather for
+// wide matrices -- measured per rank of the bench's row partition (1M rows, 16 terms
+// per row), blocked vs gather with 16K- / 32K-column bands: 1M columns
+// 47 vs 59 / -, 2M 61 vs 60 / 66, 4M 83 vs 77 / 74, 8M 145 vs - / 93 us.  Past ~1.5M
+// columns each blocked tile sweeps more x through LDS than gathering its terms' x costs.
+constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 19);   // gather kind: > 1.5M columns
+constexpr int64_t kWideCols = 3 * ((int64_t)1 << 20);     // its 32K-column bands: > 3M
 
 XbKind xband_kind_setting(const sm_matrix *m) {
     const char *e = getenv("SM_XBAND_KIND");
     if (e && strcmp(e, "exact") == 0) return kXbExact;
     if (e && strcmp(e, "gather") == 0) return kXbGather;
     if (e && strcmp(e, "blocked") == 0) return kXbBlocked;
-    return m->n_cols > kWideCols ? kXbGather : kXbBlocked;
+    return m->n_cols > kGatherCols ? kXbGather : kXbBlocked;
 }
 
 bool want_xband(const sm_matrix *m) {
@@ -158,15 +159,17 @@ bool want_xband(const sm_matrix *m) {
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
-    // Gather kind on wide slices (> 3M columns, < 0.05 terms per row per 8K columns):
-    // bands of 32K columns -- a quarter of the bands, hence of the per-band barriers, for
-    // the same terms (8M columns: 93 vs 122 us); the rank field shrinks to 3 bits, ample
-    // there.  SM_XBAND_GBAND=13|15 forces.
+    // Gather kind on wide slices: bands of 16K (> 1.5M columns) or 32K columns (> 3M) --
+    // fewer bands, hence fewer per-band barriers, for the same terms (8M columns: 93 us
+    // with 32K bands vs 122 with 8K); the rank field shrinks to 4 / 3 bits, ample at
+    // < 0.25 terms per row per band.  SM_XBAND_GBAND=13|14|15 forces.
     const char *gb = getenv("SM_XBAND_GBAND");
     const int gband_log2 = gb && atoi(gb) == 15 ? kXbGatherWideBandLog2
+                           : gb && atoi(gb) == 14 ? kXbGatherWideBandLog2 - 1
                            : gb && atoi(gb) == 13 ? kXbGatherBandLog2
-                           : m->n_cols > kWideCols ? kXbGatherWideBandLog2
-                                                                 : kXbGatherBandLog2;
+                           : m->n_cols > kWideCols   ? kXbGatherWideBandLog2
+                           : m->n_cols > kGatherCols ? kXbGatherWideBandLog2 - 1
+                                                     : kXbGatherBandLog2;
     const XbBits bits = kind == kXbExact    ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
                         : kind == kXbGather ? xb_bits(gband_log2, kXbGatherRowsLog2)
                                             : xb_bits(kXbBlockedBandLog2, kXbBlockedRowsLog2);

@@ -681,16 +681,19 @@ def test_device_encode_random_matches_host(sm, trans, rows, cols, stride, dens, 
     assert D.info()["nnz"] == H.info()["nnz"]
 
 
+@pytest.mark.parametrize("gband", [14, 15])
 @pytest.mark.parametrize("n_rows,n_cols,per_row", [(70000, 1000003, 16), (20000, 6000001, 16),
                                                    (5000, 40000, 3)])
-def test_xband_gather_wide_bands_vs_oracle(sm, n_rows, n_cols, per_row):
-    """Gather kind with 32K-column bands (3-bit ranks; AUTO's choice past 5M columns):
-    within the Σ|terms| bound, bit-identical when one slab; NaN in y dropped only by β = 0."""
+def test_xband_gather_wide_bands_vs_oracle(sm, n_rows, n_cols, per_row, gband):
+    """Gather kind with 16K- / 32K-column bands (4- / 3-bit ranks; AUTO's choice past 1.5M /
+    3M columns): within the Σ|terms| bound, bit-identical when one slab; NaN in y dropped
+    only by β = 0."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols + 11)
-    M = _with_env("SM_XBAND_GBAND", "15", lambda: _with_env("SM_XBAND_KIND", "gather", lambda: _with_env(
+    M = _with_env("SM_XBAND_GBAND", str(gband), lambda: _with_env("SM_XBAND_KIND", "gather", lambda: _with_env(
         "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))))
     info = M.info()
-    assert info["has_xband"] == 3 and info["xband_bands"] == (n_cols + 32767) // 32768, info
+    bw = 1 << gband
+    assert info["has_xband"] == 3 and info["xband_bands"] == (n_cols + bw - 1) // bw, info
     rng = np.random.default_rng(6)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
