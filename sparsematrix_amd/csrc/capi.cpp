@@ -180,8 +180,13 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     // (4 loader waves stage x), all 16 on the exact and gather kinds.
     const int entry_waves = kind == kXbBlocked ? kXbComputeWaves : threads / 64;
     if (!xband_build(rp, col, val, m->n_rows, m->n_cols, bits, entry_waves, xh,
-                     kind == kXbGather))
+                     kind == kXbGather)) {
+        // The gather kind's wide bands leave 3-4 rank bits: a matrix with longer row
+        // segments may still fit the blocked layout (5 bits, 8K-column bands).
+        if (kind == kXbGather && !getenv("SM_XBAND_KIND"))
+            return upload_xband(m, rp, col, val, kXbBlocked);
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
+    }
     XbandDev &d = m->plan.xb;
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
     int32_t n_slabs = 1;

@@ -708,3 +708,25 @@ def test_xband_gather_wide_bands_vs_oracle(sm, n_rows, n_cols, per_row, gband):
             assert np.array_equal(bits(got), bits(want)), (alpha, beta)
         else:
             assert_terms_close(got, want, absum)
+
+
+def test_wide_matrix_dense_rows_fall_back_to_blocked(sm):
+    """AUTO on a wide matrix (> 1.5M columns) whose rows pack > 14 terms into one 16K-column
+    band: the gather layout declines and the blocked layout serves it (correct results)."""
+    n_rows, n_cols = 3000, 2000000
+    lengths = np.full(n_rows, 4)
+    lengths[::50] = 30          # 30 terms inside columns [0, 16384) for every 50th row
+    rng = np.random.default_rng(31)
+    cols = [np.sort(rng.choice(16384 if L == 30 else n_cols, L, replace=False)) for L in lengths]
+    rp = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int32)
+    ci = np.concatenate(cols).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    assert M.info()["has_xband"] == 2, M.info()
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    want = oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5)
+    _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, 1.0, 0.5)
+    y = to_dev(y0)
+    M.spmv(to_dev(x), y, 1.0, 0.5)
+    assert_terms_close(to_host(y), want, absum)
