@@ -129,9 +129,9 @@ int32_t tile_nnz_setting() {
 // SM_XBAND_KIND=blocked|gather forces a kind.  Otherwise: blocked, or gather for
 // wide matrices -- measured per rank of the bench's row partition (1M rows, 16 terms
 // per row), blocked vs gather with 16K- / 32K-column bands: 1M columns
-// 47 vs 59 / -, 2M 61 vs 60 / 66, 4M 83 vs 77 / 74, 8M 145 vs - / 93 us.  Past ~1.5M
+// 46 vs 59 / -, 2M 59 vs 60 / 66, 4M 85 vs 77 / 73, 8M 145 vs - / 93 us.  Past ~3M
 // columns each blocked tile sweeps more x through LDS than gathering its terms' x costs.
-constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 19);   // gather kind: > 1.5M columns
+constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 20);   // gather kind: > 3M columns
 constexpr int64_t kWideCols = 3 * ((int64_t)1 << 20);     // its 32K-column bands: > 3M
 
 XbKind xband_kind_setting(const sm_matrix *m) {
@@ -159,7 +159,7 @@ bool want_xband(const sm_matrix *m) {
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
-    // Gather kind on wide slices: bands of 16K (> 1.5M columns) or 32K columns (> 3M) --
+    // Gather kind on wide slices: bands of 16K (> kGatherCols) or 32K columns (> 3M) --
     // fewer bands, hence fewer per-band barriers, for the same terms (8M columns: 93 us
     // with 32K bands vs 122 with 8K); the rank field shrinks to 4 / 3 bits, ample at
     // < 0.25 terms per row per band.  SM_XBAND_GBAND=13|14|15 forces.

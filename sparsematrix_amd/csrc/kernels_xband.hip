@@ -780,7 +780,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
 // LDS-staged kernel on config 2 (54 vs 48 us, DESIGN.md §3.4: the gathers and the
 // apply each add ~10 us that do not overlap the entry stream) but faster on wide
 // slices, where a blocked tile would sweep many MiB of x through LDS for few
-// terms: AUTO takes it past 1.5M columns (16K- then 32K-column bands; 8M: 93 vs 145 us,
+// terms: AUTO takes it past 3M columns (32K-column bands; 8M: 93 vs 145 us,
 // DESIGN.md §6).
 template <int N>
 __device__ __forceinline__ void pin_one(float *a) {

@@ -711,13 +711,13 @@ def test_xband_gather_wide_bands_vs_oracle(sm, n_rows, n_cols, per_row, gband):
 
 
 def test_wide_matrix_dense_rows_fall_back_to_blocked(sm):
-    """AUTO on a wide matrix (> 1.5M columns) whose rows pack > 14 terms into one 16K-column
+    """AUTO on a wide matrix (> 3M columns) whose rows pack > 6 terms into one 32K-column
     band: the gather layout declines and the blocked layout serves it (correct results)."""
-    n_rows, n_cols = 3000, 2000000
+    n_rows, n_cols = 3000, 4000000
     lengths = np.full(n_rows, 4)
-    lengths[::50] = 30          # 30 terms inside columns [0, 16384) for every 50th row
+    lengths[::50] = 30          # 30 terms inside columns [0, 32768) for every 50th row
     rng = np.random.default_rng(31)
-    cols = [np.sort(rng.choice(16384 if L == 30 else n_cols, L, replace=False)) for L in lengths]
+    cols = [np.sort(rng.choice(32768 if L == 30 else n_cols, L, replace=False)) for L in lengths]
     rp = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int32)
     ci = np.concatenate(cols).astype(np.int32)
     va = rng.uniform(-1, 1, ci.size).astype(np.float32)
