@@ -131,6 +131,12 @@ def main():
             dist.init_process_group(backend)
     smd.load()
 
+    if args.replicas < 1:
+        raise SystemExit("--replicas must be >= 1")
+    if world > 1 and not args.no_overlap and args.replicas < 2:
+        raise SystemExit("--gpus N>1 overlaps the all-gather of step k+1 with the SpMV of step k, "
+                         "which needs >= 2 replicas (distinct x buffers); use --replicas 2+ or "
+                         "--no-overlap")
     R = args.rows_per_rank
     emu = args.emulate_world if world == 1 and args.emulate_world > 1 else 1
     C = R * world * emu                    # global columns (= global rows)

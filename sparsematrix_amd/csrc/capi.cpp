@@ -132,7 +132,6 @@ int32_t tile_nnz_setting() {
 // 46 vs 59 / -, 2M 59 vs 60 / 66, 4M 85 vs 77 / 73, 8M 145 vs - / 93 us.  Past ~3M
 // columns each blocked tile sweeps more x through LDS than gathering its terms' x costs.
 constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 20);   // gather kind: > 3M columns
-constexpr int64_t kWideCols = 3 * ((int64_t)1 << 20);     // its 32K-column bands: > 3M
 
 XbKind xband_kind_setting(const sm_matrix *m) {
     const char *e = getenv("SM_XBAND_KIND");
@@ -142,12 +141,9 @@ XbKind xband_kind_setting(const sm_matrix *m) {
     return m->n_cols > kGatherCols ? kXbGather : kXbBlocked;
 }
 
-bool want_xband(const sm_matrix *m) {
-    const char *e = getenv("SM_XBAND");
-    if (e && atoi(e) == 0) return false;
-    if (m->nnz == 0 || m->n_rows == 0) return false;
-    if (e && atoi(e) == 1) return true;
-    const XbKind kind = xband_kind_setting(m);
+// Sweeping x through LDS (or walking its bands) pays when the L2 -> LDS bytes of
+// one kind's row blocks stay within 20x the matrix stream.
+static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
                           : kind == kXbGather ? kXbGatherRowsLog2
                                               : kXbBlockedRowsLog2;
@@ -157,18 +153,27 @@ bool want_xband(const sm_matrix *m) {
     return x_sweep <= 20.0 * stream && m->n_cols >= 8192;
 }
 
+bool want_xband(const sm_matrix *m) {
+    const char *e = getenv("SM_XBAND");
+    if (e && atoi(e) == 0) return false;
+    if (m->nnz == 0 || m->n_rows == 0) return false;
+    if (e && atoi(e) == 1) return true;
+    return xband_cost_ok(m, xband_kind_setting(m));
+}
+
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
-    // Gather kind on wide slices: bands of 16K (> kGatherCols) or 32K columns (> 3M) --
-    // fewer bands, hence fewer per-band barriers, for the same terms (8M columns: 93 us
-    // with 32K bands vs 122 with 8K); the rank field shrinks to 4 / 3 bits, ample at
-    // < 0.25 terms per row per band.  SM_XBAND_GBAND=13|14|15 forces.
+    // Gather kind: AUTO takes it past kGatherCols (3M columns) with bands of 32K
+    // columns -- fewer bands, hence fewer per-band barriers, for the same terms (8M
+    // columns: 93 us with 32K bands vs 122 with 8K); the rank field shrinks to 3 bits,
+    // ample at < 0.25 terms per row per band.  A forced gather kind on a narrower
+    // matrix (SM_XBAND_KIND=gather) keeps 8K-column bands.  SM_XBAND_GBAND=13|14|15
+    // forces the band width (16K: measured slower than the blocked kind at 2M).
     const char *gb = getenv("SM_XBAND_GBAND");
     const int gband_log2 = gb && atoi(gb) == 15 ? kXbGatherWideBandLog2
                            : gb && atoi(gb) == 14 ? kXbGatherWideBandLog2 - 1
                            : gb && atoi(gb) == 13 ? kXbGatherBandLog2
-                           : m->n_cols > kWideCols   ? kXbGatherWideBandLog2
-                           : m->n_cols > kGatherCols ? kXbGatherWideBandLog2 - 1
+                           : m->n_cols > kGatherCols ? kXbGatherWideBandLog2
                                                      : kXbGatherBandLog2;
     const XbBits bits = kind == kXbExact    ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
                         : kind == kXbGather ? xb_bits(gband_log2, kXbGatherRowsLog2)
@@ -183,7 +188,10 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
                      kind == kXbGather)) {
         // The gather kind's wide bands leave 3-4 rank bits: a matrix with longer row
         // segments may still fit the blocked layout (5 bits, 8K-column bands).
-        if (kind == kXbGather && !getenv("SM_XBAND_KIND"))
+        // Only where the blocked kind's own sweep cost still pays (its row blocks
+        // differ from the gather kind's); otherwise the stream kernel serves it.
+        if (kind == kXbGather && !getenv("SM_XBAND_KIND") &&
+            (xband_cost_ok(m, kXbBlocked) || getenv("SM_XBAND")))
             return upload_xband(m, rp, col, val, kXbBlocked);
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     }
@@ -191,7 +199,8 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     // Blocked: split the bands in slabs so there are >= kXbTargetTiles tiles.
     int32_t n_slabs = 1;
     if (kind != kXbExact) {
-        const int64_t want = (target_tiles + xh.n_blocks - 1) / xh.n_blocks;
+        // At most 64 slabs: the hand-off counts arrivals in 8 bits (kernels_xband.hip).
+        const int64_t want = std::min<int64_t>(64, (target_tiles + xh.n_blocks - 1) / xh.n_blocks);
         n_slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(want, xh.n_bands));
     }
     // Slabs of whole groups of 8 bands (the kernel steps bands 4 or 8 at a time).
@@ -206,8 +215,9 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     if (n_slabs > 1) {
         const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(n_slabs - 1) * ps, m->device_bytes));
-        SM_TRY_HIP(dev_alloc(&d.d_tickets, xh.n_blocks, m->device_bytes));
-        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)xh.n_blocks * sizeof(int32_t)));
+        // Slab hand-off control words (kernels_xband.hip: started, arrive, done, pad).
+        SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)xh.n_blocks, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)xh.n_blocks * 4 * sizeof(int32_t)));
     }
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, cs32.data(), cs32.size() * 4, hipMemcpyHostToDevice));
     if (!xh.word.empty()) {

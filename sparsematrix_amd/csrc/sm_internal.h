@@ -45,7 +45,7 @@ struct XbandDev {
     uint32_t *d_word = nullptr;
     float *d_val = nullptr;
     float *d_partials = nullptr;      // (n_slabs - 1) * n_rows slab partial sums (one SpMV in flight)
-    int32_t *d_tickets = nullptr;     // n_blocks slab-completion counters, zero between SpMVs
+    int32_t *d_tickets = nullptr;     // 4 x n_blocks slab hand-off control words, zero between SpMVs
 };
 
 struct Plan {

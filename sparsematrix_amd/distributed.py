@@ -45,6 +45,15 @@ def allgather_spmv(local_spmv: Callable, x_local, x_full, y_local, group=None):
     return local_spmv(x_full, y_local)
 
 
+def _same_buffer(a, b) -> bool:
+    """True when two tensors/arrays overlap in memory (same storage start)."""
+    pa = a.data_ptr() if hasattr(a, "data_ptr") else a.__array_interface__["data"][0]
+    pb = b.data_ptr() if hasattr(b, "data_ptr") else b.__array_interface__["data"][0]
+    na = a.numel() * a.element_size() if hasattr(a, "numel") else a.nbytes
+    nb = b.numel() * b.element_size() if hasattr(b, "numel") else b.nbytes
+    return pa < pb + nb and pb < pa + na
+
+
 def allgather_spmv_pipelined(products, group=None):
     """A sequence of independent products, each `(local_spmv, x_local, x_full,
     y_local)`: the all-gather of product k+1 is in flight while product k's SpMV
@@ -68,6 +77,10 @@ def allgather_spmv_pipelined(products, group=None):
         cur_work.wait()
         nxt = next(it, None)
         if nxt is not None:
+            if _same_buffer(nxt[2], cur[2]):
+                raise ValueError("allgather_spmv_pipelined: consecutive products share one "
+                                 "x_full buffer; the all-gather of product k+1 would overwrite "
+                                 "x while SpMV k reads it (rotate at least two x_full buffers)")
             work = dist.all_gather_into_tensor(nxt[2], nxt[1], group=group, async_op=True)
         cur[0](cur[2], cur[3])
         n += 1
