@@ -65,11 +65,12 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather"}
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "exact": "spmv_xband_kernel (exact band layout)",
            "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)",
-           "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)"}
+           "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)",
+           "band2": "spmv_band2_kernel (balanced bands, distributed slab combine)"}
 
 
 def load_traffic(workload: str, layout: str):

@@ -94,14 +94,16 @@ typedef struct sm_info {
     int32_t n_long_rows;        /* rows split across workgroups                */
     int32_t max_row_nnz;        /* longest row                                 */
     int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
-                                   2 blocked (column slabs, Σ|terms| tolerance)  */
+                                   2 blocked, 3 gather, 4 band2 (balanced bands);
+                                   2-4 sum each column slab in the reference's
+                                   order and add the slab sums in slab order     */
     int32_t xband_blocks, xband_bands;
     int32_t xband_slabs;        /* column slabs per row block (1: bit-identical) */
     int32_t xband_block_rows;   /* rows per block                              */
     int64_t device_bytes;       /* device memory held by the matrix            */
     int32_t col_relabel;        /* 1: the stream SpMV gathers x through a column
                                    relabeling by descending degree (skewed graphs) */
-    int32_t reserved;
+    int32_t xband_slab_cols;    /* columns per slab (slab s = [s*c, (s+1)*c))   */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */

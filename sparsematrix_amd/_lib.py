@@ -51,7 +51,7 @@ class SmInfo(C.Structure):
         ("device", C.c_int32), ("n_tiles", C.c_int32), ("n_long_rows", C.c_int32),
         ("max_row_nnz", C.c_int32), ("has_xband", C.c_int32), ("xband_blocks", C.c_int32),
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
-        ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("reserved", C.c_int32),
+        ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
     ]
 
 

@@ -1,0 +1,201 @@
+// band2.cpp -- host-side builder of the balanced-band layout used by
+// spmv_band2_kernel (kernels_band2.hip).  Layout: xband.h (Band2Host).
+//
+// Per tile (block b of rows, slab s of columns) the builder walks the slab's
+// columns left to right and closes a band [clo, chi) as soon as either
+//   * its window from clo rounded down to 4 columns would pass kB2Window columns,
+//   * its terms, packed row by row into 64-entry chunks without splitting a row's
+//     segment (the row's run of terms inside the band), would need more than
+//     kB2Chunks chunks, or
+//   * a row would have more than 14 terms in it (the 4-bit rank field),
+// so every band is one fixed-size slot of 32 chunks: the kernel's wave w applies
+// chunks 2w and 2w+1 and loads them with one 16-byte load per lane.  Columns
+// without terms never open a band.  Inside a band the terms are listed by row,
+// each row's segment in ascending column order, so across the tile's bands (which
+// ascend in column) every row's terms are added in the reference's order
+// (sparse-matrix.cc:164-190, kernel.cc:780-796: per output, ascending column).
+#include <algorithm>
+#include <thread>
+
+#include "xband.h"
+
+namespace smamd {
+
+namespace {
+
+struct TileOut {
+    std::vector<int32_t> clo;
+    std::vector<uint32_t> ent;
+    int64_t terms = 0;
+    bool ok = true;
+};
+
+struct Seg {
+    int32_t rl, s, n;   // row in block, first term, count
+};
+
+// Lanes inside a chunk: segments of 2+ terms take consecutive lanes first (the
+// kernel passes a running sum up the lanes), then each single term of row r goes
+// to lane r mod 32 or 32 + r mod 32 when free -- so the 32 lanes of each half
+// read and write their accumulators in 32 distinct LDS banks -- else the highest
+// free lane.
+void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const int32_t *col,
+                const float *val, int32_t clo_al) {
+    bool used[64] = {false};
+    int next = 0;
+    const int wave = c >> 1, k = c & 1;
+    auto put = [&](const Seg &g, int32_t j, int lane) {
+        uint32_t *e = band_ent + ((size_t)(wave * 64 + lane)) * 4;
+        const uint32_t cb = (uint32_t)(col[g.s + j] - clo_al);
+        e[k] = (cb | ((uint32_t)j << kB2ColBits) | ((uint32_t)g.rl << (kB2ColBits + kB2RankBits))) ^
+               kB2DummyWord;
+        float v = val[g.s + j];
+        uint32_t vb;
+        __builtin_memcpy(&vb, &v, 4);
+        e[2 + k] = vb;
+        used[lane] = true;
+    };
+    for (const Seg &g : segs)
+        if (g.n > 1)
+            for (int32_t j = 0; j < g.n; j++) put(g, j, next++);
+    for (const Seg &g : segs) {
+        if (g.n != 1) continue;
+        const int bank = g.rl & 31;
+        int lane = !used[bank] ? bank : !used[32 + bank] ? 32 + bank : -1;
+        if (lane < 0)
+            for (lane = 63; used[lane]; lane--) {}
+        put(g, 0, lane);
+    }
+}
+
+void build_tile(const int32_t *rp, const int32_t *col, const float *val, int64_t r0, int64_t r1,
+                int64_t c0, int64_t c1, TileOut &out) {
+    const int64_t nr = r1 - r0;
+    std::vector<int32_t> cur((size_t)nr), end((size_t)nr);
+    std::vector<int32_t> hist((size_t)(c1 - c0) + 1, 0);
+    for (int64_t r = r0; r < r1; r++) {
+        const int32_t *a = col + rp[r], *z = col + rp[r + 1];
+        cur[r - r0] = (int32_t)(std::lower_bound(a, z, (int32_t)c0) - col);
+        end[r - r0] = (int32_t)(std::lower_bound(a, z, (int32_t)c1) - col);
+        for (int32_t e = cur[r - r0]; e < end[r - r0]; e++) hist[(size_t)(col[e] - c0)]++;
+    }
+    // hist -> prefix counts H[i] = terms in columns [c0, c0 + i)
+    std::vector<int64_t> H((size_t)(c1 - c0) + 1, 0);
+    for (int64_t i = 0; i < c1 - c0; i++) H[(size_t)i + 1] = H[(size_t)i] + hist[(size_t)i];
+    auto count = [&](int64_t a, int64_t b) { return H[(size_t)(b - c0)] - H[(size_t)(a - c0)]; };
+    int64_t clo = c0;
+    std::vector<Seg> segs;
+    std::vector<std::vector<Seg>> chunk_segs;
+    while (clo < c1 && count(clo, c1) > 0) {
+        while (hist[(size_t)(clo - c0)] == 0) clo++;   // no band starts on an empty column
+        const int64_t clo_al = clo & ~(int64_t)3;
+        const int64_t lim = std::min<int64_t>(c1, clo_al + kB2Window);
+        // Largest chi <= lim with at most 32 * 64 terms (binary search on H).
+        int64_t lo = clo + 1, hi = lim;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) / 2;
+            if (count(clo, mid) <= (int64_t)kB2Chunks * 64) lo = mid; else hi = mid - 1;
+        }
+        int64_t chi = lo;
+        for (;;) {   // pack; shrink chi until the band fits
+            segs.clear();
+            bool retry = false;
+            int chunks = 0, fill = 64;
+            for (int64_t r = 0; r < nr && !retry; r++) {
+                const int32_t s = cur[(size_t)r];
+                int32_t n = 0;
+                while (s + n < end[(size_t)r] && col[s + n] < chi) n++;
+                if (n == 0) continue;
+                if (n > (int32_t)kB2DummyRank - 1) {   // ranks 0..13 + dummy 15: cut the band
+                    chi = col[s + kB2DummyRank - 1];
+                    retry = true;
+                    break;
+                }
+                if (fill + n > 64) { chunks++; fill = 0; }
+                fill += n;
+                segs.push_back(Seg{(int32_t)r, s, n});
+            }
+            if (retry) continue;
+            if (chunks > kB2Chunks) {
+                chi = clo + std::max<int64_t>(1, (chi - clo) * 31 / 32);
+                continue;
+            }
+            break;
+        }
+        // Emit: segments into chunks in row order.
+        const size_t base = out.ent.size();
+        out.ent.resize(base + 4096, 0u);   // dummies: word 0 (= dummy ^ dummy), value 0
+        out.clo.push_back((int32_t)clo_al);
+        chunk_segs.assign(kB2Chunks, {});
+        int c = -1, fill = 64;
+        for (const Seg &g : segs) {
+            if (fill + g.n > 64) { c++; fill = 0; }
+            fill += g.n;
+            chunk_segs[(size_t)c].push_back(g);
+            cur[(size_t)g.rl] += g.n;
+            out.terms += g.n;
+        }
+        for (int k = 0; k <= c; k++)
+            emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, (int32_t)clo_al);
+        clo = chi;
+    }
+    for (int64_t r = 0; r < nr; r++)
+        if (cur[(size_t)r] != end[(size_t)r]) out.ok = false;   // unsorted columns
+}
+
+}  // namespace
+
+bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out) {
+    out = Band2Host();
+    if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
+    for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
+        for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)
+            if (col[e] <= col[e - 1]) return false;
+    const int32_t br = (int32_t)std::min<int64_t>(kB2BlockRows, n_rows);
+    const int64_t nblk = (n_rows + br - 1) / br;
+    // Slabs of whole 256-column pieces.
+    const int64_t sc = ((n_cols + n_slabs - 1) / n_slabs + 255) & ~(int64_t)255;
+    const int64_t ns = (n_cols + sc - 1) / sc;
+    const int64_t ntile = nblk * ns;
+    if (ntile >= ((int64_t)1 << 30)) return false;
+    std::vector<TileOut> tiles((size_t)ntile);
+    const int nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++)
+        th.emplace_back([&, t] {
+            for (int64_t i = t; i < ntile; i += nthr) {
+                const int64_t b = i / ns, s = i % ns;
+                build_tile(rp, col, val, b * br, std::min<int64_t>(n_rows, (b + 1) * br), s * sc,
+                           std::min<int64_t>(n_cols, (s + 1) * sc), tiles[(size_t)i]);
+            }
+        });
+    for (auto &x : th) x.join();
+    out.block_rows = br;
+    out.n_blocks = (int32_t)nblk;
+    out.n_slabs = (int32_t)ns;
+    out.slab_cols = (int32_t)sc;
+    out.tile_band_start.resize((size_t)ntile + 1);
+    int64_t nb = 0;
+    for (int64_t i = 0; i < ntile; i++) {
+        if (!tiles[(size_t)i].ok) return false;
+        out.tile_band_start[(size_t)i] = (int32_t)nb;
+        const int64_t k = (int64_t)tiles[(size_t)i].clo.size();
+        out.max_bands_per_tile = std::max<int32_t>(out.max_bands_per_tile, (int32_t)k);
+        nb += k;
+        out.real_terms += tiles[(size_t)i].terms;
+    }
+    out.tile_band_start[(size_t)ntile] = (int32_t)nb;
+    if (nb * 4096 >= ((int64_t)1 << 31)) return false;   // 32-bit entry offsets (x 4 bytes per dword)
+    out.n_bands = nb;
+    out.band_clo.reserve((size_t)nb);
+    out.ent.reserve((size_t)nb * 4096);
+    for (auto &t : tiles) {
+        out.band_clo.insert(out.band_clo.end(), t.clo.begin(), t.clo.end());
+        out.ent.insert(out.ent.end(), t.ent.begin(), t.ent.end());
+        std::vector<uint32_t>().swap(t.ent);
+    }
+    return true;
+}
+
+}  // namespace smamd

@@ -84,6 +84,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.xb.d_val);
     (void)hipFree(m->plan.xb.d_partials);
     (void)hipFree(m->plan.xb.d_tickets);
+    (void)hipFree(m->plan.xb.d_band_clo);
     (void)hipFree(m->plan.d_perm);
     (void)hipFree(m->plan.d_rcol);
     (void)hipFree(m->plan.d_xperm);
@@ -126,7 +127,9 @@ int32_t tile_nnz_setting() {
 // (~22 TB/s chip-wide) while 4-byte gathers run at 75-200 G/s by the size of x,
 // so the sweep wins while its bytes stay under ~20x the matrix's 8 B per term.
 // SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
-// SM_XBAND_KIND=blocked|gather forces a kind.  Otherwise: blocked, or gather for
+// SM_XBAND_KIND=blocked|gather|band2 forces a kind.  Otherwise: band2 (balanced
+// bands, kernels_band2.hip: config 2 41.1 us vs 41.7 blocked, bit-identical; it
+// falls back to blocked when its bands would be < 70 % filled), or gather for
 // wide matrices -- measured per rank of the bench's row partition (1M rows, 16 terms
 // per row), blocked vs gather with 16K- / 32K-column bands: 1M columns
 // 46 vs 59 / -, 2M 59 vs 60 / 66, 4M 85 vs 77 / 73, 8M 145 vs - / 93 us.  Past ~3M
@@ -138,13 +141,17 @@ XbKind xband_kind_setting(const sm_matrix *m) {
     if (e && strcmp(e, "exact") == 0) return kXbExact;
     if (e && strcmp(e, "gather") == 0) return kXbGather;
     if (e && strcmp(e, "blocked") == 0) return kXbBlocked;
-    return m->n_cols > kGatherCols ? kXbGather : kXbBlocked;
+    if (e && strcmp(e, "band2") == 0) return kXbBand2;
+    // band2 (balanced bands) where its bands fill: it declines to the blocked kind
+    // when they would be mostly padding (upload_band2).
+    return m->n_cols > kGatherCols ? kXbGather : kXbBand2;
 }
 
 // Sweeping x through LDS (or walking its bands) pays when the L2 -> LDS bytes of
 // one kind's row blocks stay within 20x the matrix stream.
 static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
+                          : kind == kXbBand2  ? kB2RowBits
                           : kind == kXbGather ? kXbGatherRowsLog2
                                               : kXbBlockedRowsLog2;
     const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
@@ -161,8 +168,67 @@ bool want_xband(const sm_matrix *m) {
     return xband_cost_ok(m, xband_kind_setting(m));
 }
 
+// Balanced-band layout (band2.cpp, kernels_band2.hip): slabs so there are about
+// kXbTargetTiles tiles of <= 16K rows.
+static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
+                              const float *val) {
+    const int64_t br = std::min<int64_t>(kB2BlockRows, m->n_rows);
+    const int64_t nblk = (m->n_rows + br - 1) / br;
+    int32_t want = (int32_t)std::max<int64_t>(
+        1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
+    if (const char *e = getenv("SM_BAND2_SLABS"))   // development / tests: force the slab count
+        want = std::max(1, std::min(16, atoi(e)));
+    Band2Host bh;
+    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh)) return SM_OK;
+    // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
+    // dummies (wide or very sparse matrices), the padding would cost more HBM bytes
+    // than the layout saves -- decline unless forced (SM_XBAND_KIND=band2).
+    const char *kind_env = getenv("SM_XBAND_KIND");
+    const bool forced = kind_env && strcmp(kind_env, "band2") == 0;
+    if (!forced && bh.n_bands > 0 &&
+        (double)bh.real_terms < 0.7 * (double)bh.n_bands * kB2Chunks * 64)
+        return SM_OK;
+    XbandDev &d = m->plan.xb;
+    const int64_t ntile = (int64_t)bh.n_blocks * bh.n_slabs;
+    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, bh.n_bands), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, bh.n_bands * 4096), m->device_bytes));
+    if (bh.n_slabs > 1) {
+        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
+        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(bh.n_slabs - 1) * ps, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)bh.n_blocks, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)bh.n_blocks * 4 * sizeof(int32_t)));
+    }
+    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, bh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
+                         hipMemcpyHostToDevice));
+    if (bh.n_bands > 0) {
+        SM_TRY_HIP(hipMemcpy(d.d_band_clo, bh.band_clo.data(), (size_t)bh.n_bands * 4,
+                             hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_word, bh.ent.data(), (size_t)bh.n_bands * 4096 * 4,
+                             hipMemcpyHostToDevice));
+    }
+    d.kind = kXbBand2;
+    d.threads = 1024;
+    d.block_rows = bh.block_rows;
+    d.band_cols = kB2Window;
+    d.n_bands = (int32_t)std::min<int64_t>(bh.n_bands, INT32_MAX);
+    d.n_slabs = bh.n_slabs;
+    d.slab_bands = bh.slab_cols;
+    d.n_chunks = bh.n_bands * kB2Chunks;
+    d.max_chunks_per_band = bh.max_bands_per_tile;
+    d.n_blocks = bh.n_blocks;
+    return SM_OK;
+}
+
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
+    if (kind == kXbBand2) {
+        const sm_status st = upload_band2(m, rp, col, val);
+        const char *e = getenv("SM_XBAND_KIND");
+        if (st == SM_OK && m->plan.xb.n_blocks == 0 && !(e && strcmp(e, "band2") == 0))
+            return upload_xband(m, rp, col, val, kXbBlocked);   // declined: blocked kind
+        return st;
+    }
     // Gather kind: AUTO takes it past kGatherCols (3M columns) with bands of 32K
     // columns -- fewer bands, hence fewer per-band barriers, for the same terms (8M
     // columns: 93 us with 32K bands vs 122 with 8K); the rank field shrinks to 3 bits,
@@ -695,6 +761,10 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->xband_bands = m->plan.xb.n_bands;
     info->xband_slabs = m->plan.xb.n_blocks > 0 ? m->plan.xb.n_slabs : 0;
     info->xband_block_rows = m->plan.xb.block_rows;
+    info->xband_slab_cols =
+        m->plan.xb.n_blocks == 0 ? 0
+        : m->plan.xb.kind == kXbBand2 ? m->plan.xb.slab_bands   // band2 keeps slab columns there
+        : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     return SM_OK;
@@ -798,7 +868,9 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     case SM_ALGO_AUTO:
     case SM_ALGO_XBAND:
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
-            e = launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
+            e = m->plan.xb.kind == kXbBand2
+                    ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
+                    : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
             break;
         }
         // fall through: no band layout (or unaligned x) -> stream kernel

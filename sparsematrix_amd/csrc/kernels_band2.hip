@@ -1,0 +1,300 @@
+// kernels_band2.hip -- SpMV over the balanced-band layout (band2.cpp, xband.h).
+//
+// One workgroup (1024 threads, 16 waves) per tile = (block of <= 16384 rows, slab
+// of columns), one per CU.  A tile's bands are column windows of <= 8192 columns
+// holding exactly 32 chunks of 64 entries (dummies pad the last): wave w applies
+// chunks 2w and 2w+1 of every band, and gets both -- two words, two values -- with
+// one 16-byte load per lane.  LDS: two x windows (double-buffered) and the block's
+// accumulators.
+//
+// Per band p, every wave (static register rings, the loop unrolled by 6):
+//   load x window p+6 into registers (two float4 per lane),
+//   store x window p+1 (loaded five bands ago) into the free LDS buffer,
+//   apply band p: term = x_lds[col] * (v * alpha), the chunk's terms added to the
+//   LDS accumulators in rank rounds (a row's segment runs up consecutive lanes by
+//   DPP, its last lane writes; no two lanes touch one row in a round, no atomics),
+//   load the entries of band p+6 (into the registers band p's entries held),
+//   barrier.
+// Why x goes through registers rather than LDS-DMA: vmcnt retires in issue order,
+// so a wave that waits for an LDS-DMA issued this band also waits for every entry
+// load it issued before -- the entry prefetch would collapse to one band.  Loaded
+// into registers six bands ahead, the x windows are waited for only when they are
+// old, and five bands of entries (80 KiB per CU) stay in flight.
+//
+// Summation order: bands ascend in column, a row's terms inside a band ascend in
+// column (ranks), so inside a tile every row is summed in the reference's order
+// (kernel.cc:780-796, per output ascending column); slab 0 starts from beta*y,
+// later slabs from -0.0, and the slab sums are added in slab order by the slab
+// hand-off (xband_dev.h) -- bit-identical to the reference with one slab, within
+// the Sum|terms| bound otherwise, deterministic always.
+#include "sm_internal.h"
+#include "xband.h"
+#include "xband_dev.h"
+
+#include <cstdlib>
+
+namespace smamd {
+namespace {
+
+constexpr int kB2Threads = 1024;
+
+// ABL (development only, SM_BAND2_ABLATE; results wrong): 1 skips the apply,
+// 2 the x loads and stores, 4 the entry loads, 8 the slab hand-off (plain stores),
+// 16 the band loop.
+template <int ABL, int PRIO>
+__global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
+    int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
+    const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
+    const uint32_t *__restrict__ ent, const float *__restrict__ x, float *__restrict__ y,
+    float *__restrict__ partials, int32_t *__restrict__ ctl, float alpha, float beta) {
+    constexpr int BROWS = kB2BlockRows;
+    constexpr int W = kB2Window;
+    constexpr uint32_t kColMask = (1u << kB2ColBits) - 1u;
+    constexpr uint32_t kRankMask = (1u << kB2RankBits) - 1u;
+    // Rings: x window p+A and the entries of band p+A are loaded at band p into the
+    // slots band p just freed (the x of window p was stored a band ago; the entries
+    // of band p are loaded after its apply has decoded them).  Waiting for window p+1
+    // (loaded A-1 bands ago) retires every older load, so A bands of entries stay in
+    // flight: A = 6 keeps ~80 KiB per CU on the way from HBM.
+    constexpr int A = 6;            // lookahead = ring size = loop unroll
+    static_assert(W == 2 * 4 * kB2Threads, "two float4 of x per lane per band");
+    __shared__ __attribute__((aligned(16))) float xs[2][W];
+    __shared__ __attribute__((aligned(16))) float yacc[BROWS + 64];   // + a scratch slot per lane
+    __shared__ int32_t s_word[4];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int32_t t = blockIdx.x;
+    const int32_t b = t / n_slabs;
+    const int32_t slab = t - b * n_slabs;
+    if (!(ABL & 8)) handoff_started(ctl + (int64_t)b * kCtlWords, n_slabs);
+    const int32_t g0 = tile_band_start[t];
+    const int32_t nb = tile_band_start[t + 1] - g0;
+    const int32_t r0 = b * block_rows;
+    const int32_t nr = min(block_rows, n_rows - r0);
+    const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
+    const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * 4096, (uint64_t)nb * 16384);
+    // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi), read
+    // by readlane; the window advances by 64 bands when the x loads reach its hi half.
+    const int32_t *clg = band_clo + g0;
+    int32_t cw = 0;
+    int32_t clo_lo = lane < nb ? clg[lane] : 0;
+    int32_t clo_hi = 64 + lane < nb ? clg[64 + lane] : 0;
+    auto clo_at = [&](int32_t q) -> int32_t {   // q in [cw, cw + 128), wave-uniform
+        const int32_t j = q - cw;
+        const int32_t lo = __builtin_amdgcn_readlane(clo_lo, j & 63);
+        const int32_t hi = __builtin_amdgcn_readlane(clo_hi, j & 63);
+        return j < 64 ? lo : hi;
+    };
+    auto advance = [&]() {
+        cw += 64;
+        clo_lo = clo_hi;
+        clo_hi = cw + 64 + lane < nb ? clg[cw + 64 + lane] : 0;
+    };
+
+    // x window q: float4 slots tid and tid + 1024 of [clo_q, clo_q + 8192); windows
+    // past the tile read nothing (offset past the descriptor).
+    auto load_x = [&](int32_t q, float4 *xr) {
+        const int32_t c = q < nb ? clo_at(q) : 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t off = q < nb ? 4u * (uint32_t)(c + 4 * (tid + k * kB2Threads)) : 0xFFFFFFF0u;
+            u32x4 v = {off, off, off, off};
+            if (!(ABL & 2)) v = __builtin_amdgcn_raw_buffer_load_b128(x_src, off, 0, 0);
+            xr[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                                __uint_as_float(v.w));
+        }
+    };
+    auto store_x = [&](int buf, const float4 *xr) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ABL & 2)
+                asm volatile("" ::"v"(xr[k].x), "v"(xr[k].y), "v"(xr[k].z), "v"(xr[k].w));
+            else
+                *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * kB2Threads)]) = xr[k];
+        }
+    };
+    // Entries of band q: {word 2w, word 2w+1, value 2w, value 2w+1} for this lane;
+    // past the tile: zeros = dummies.
+    auto load_e = [&](int32_t q) -> u32x4 {
+        const uint32_t off = 16384u * (uint32_t)q + 16u * (uint32_t)tid;
+        if (ABL & 4) return u32x4{0u, 0u, 0u, 0u};
+        return __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, kAuxNt);
+    };
+
+    auto shr1 = [](float v) {   // lane i <- lane i-1 (lane 0 never has rank >= 1)
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+    };
+    auto shl1 = [](uint32_t v) {   // lane i <- lane i+1; lane 63 <- the dummy rank
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)kB2DummyRank, (int)v, 0x130, 0xF, 0xF, false);
+    };
+    auto apply = [&](const float *xb, u32x4 e) {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        const uint32_t wd[2] = {e.x ^ kB2DummyWord, e.y ^ kB2DummyWord};
+        const float va[2] = {__uint_as_float(e.z), __uint_as_float(e.w)};
+        float xv[2], yv[2];
+        uint32_t rk[2], rl[2];
+        bool live[2];
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            rk[k] = (wd[k] >> kB2ColBits) & kRankMask;
+            live[k] = rk[k] != kB2DummyRank;
+            rl[k] = wd[k] >> (kB2ColBits + kB2RankBits);   // dummies decode to row 0, column 0
+            xv[k] = xb[wd[k] & kColMask];
+            yv[k] = yacc[rl[k]];
+            more |= live[k] && rk[k] > 0;
+        }
+        // Materialise all four reads before any write (one LDS wait per band).
+        asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]));
+        float tm[2], acc[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            tm[k] = __fmul_rn(xv[k], __fmul_rn(va[k], alpha));
+            acc[k] = __fadd_rn(yv[k], tm[k]);
+        }
+        if (__any(more)) {
+            for (uint32_t r = 1;; ++r) {
+                bool again = false;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const float prev = shr1(acc[k]);
+                    if (rk[k] == r) acc[k] = __fadd_rn(prev, tm[k]);
+                    again |= live[k] && rk[k] > r;
+                }
+                if (!__any(again)) break;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {   // every lane writes: the segment's last to its row
+            const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
+            yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
+        }
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    };
+
+    // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row
+    // without terms in this slab keeps the sign of a zero y), all loads in flight.
+    constexpr int kQ = BROWS / (4 * kB2Threads);
+    const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
+    if (slab == 0) {
+        const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
+        float4 v[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint32_t o = 16u * (uint32_t)(tid + q * kB2Threads);
+            if (y_vec) {
+                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(yi_src, o, 0, 0);
+                v[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                   __uint_as_float(u.z), __uint_as_float(u.w));
+            } else {
+                v[q] = make_float4(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 4, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 8, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 12, 0, 0)));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (beta != 1.0f)
+                v[q] = make_float4(__fmul_rn(v[q].x, beta), __fmul_rn(v[q].y, beta),
+                                   __fmul_rn(v[q].z, beta), __fmul_rn(v[q].w, beta));
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = v[q];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
+    }
+
+    // Rings with static roles: x window q in X[q % A], entries of band q in E[q % A].
+    // Prologue = virtual bands -A..-1 (their loads in the loop's order), so the loads
+    // pending at the loop header are in the order the loop's back edge leaves them.
+    float4 X[A][2];
+    u32x4 E[A];
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+        load_x(q, X[q]);
+        E[q] = load_e(q);
+    }
+    store_x(0, X[0]);
+    __syncthreads();
+
+    // Whole groups of A bands (static ring indices, no branch around a load or a
+    // ring register: either makes hipcc copy registers and drain vmcnt).  Steps past
+    // the tile's last band see only dummy entries (their loads go past the
+    // descriptors: no memory request) and skip the barrier -- a uniform branch; the
+    // dummies only write the scratch slots and the x buffers nobody reads any more.
+    const int32_t nbu = (ABL & 16) ? 0 : (nb + A - 1) / A * A;
+    for (int32_t p = 0; p < nbu; p += A) {
+#pragma unroll
+        for (int u = 0; u < A; ++u) {
+            const int32_t q = p + u;
+            if (q + A >= cw + 64) advance();
+            load_x(q + A, X[u]);
+            store_x((u + 1) & 1, X[(u + 1) % A]);
+            if (ABL & 1)
+                asm volatile("" ::"v"(E[u].x), "v"(E[u].y), "v"(E[u].z), "v"(E[u].w));
+            else
+                apply(xs[u & 1], E[u]);
+            E[u] = load_e(q + A);
+            if (q < nb) __syncthreads();
+        }
+    }
+
+    if (n_slabs == 1 || (ABL & 8)) {
+        const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int32_t i = 4 * (tid + q * kB2Threads);
+            if (i < nv) *reinterpret_cast<float4 *>(y + r0 + i) = *reinterpret_cast<const float4 *>(&yacc[i]);
+        }
+        for (int32_t i = nv + tid; i < nr; i += kB2Threads) y[r0 + i] = yacc[i];
+        return;
+    }
+    slab_handoff<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
+                             nr, slab, n_slabs, y_vec);
+}
+
+}  // namespace
+
+hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                             float *y, float alpha, float beta, hipStream_t s) {
+    if (xb.n_blocks <= 0) return hipSuccess;
+    if (xb.kind != kXbBand2 || xb.n_slabs < 1 || xb.block_rows > kB2BlockRows ||
+        !xb.d_chunk_start || !xb.d_band_clo || (xb.n_bands > 0 && !xb.d_word) ||
+        (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
+        return hipErrorInvalidValue;
+    static const int abl = [] {
+        const char *e = getenv("SM_BAND2_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    static const int prio = [] {
+        const char *e = getenv("SM_BAND2_PRIO");
+        return e ? atoi(e) : 2;
+    }();
+    const dim3 grid((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), block(kB2Threads);
+#define SM_B2(A, P)                                                                            \
+    hipLaunchKernelGGL((spmv_band2_kernel<A, P>), grid, block, 0, s, n_rows, n_cols,          \
+                       xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, \
+                       y, xb.d_partials, xb.d_tickets, alpha, beta)
+    switch (abl) {
+    case 0:
+        if (prio == 0) SM_B2(0, 0); else SM_B2(0, 2);
+        break;
+    case 1: SM_B2(1, 2); break;
+    case 2: SM_B2(2, 2); break;
+    case 3: SM_B2(3, 2); break;
+    case 4: SM_B2(4, 2); break;
+    case 7: SM_B2(7, 2); break;
+    case 8: SM_B2(8, 2); break;
+    case 15: SM_B2(15, 2); break;
+    case 16: SM_B2(16, 2); break;
+    case 31: SM_B2(31, 2); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef SM_B2
+    return hipGetLastError();
+}
+
+}  // namespace smamd

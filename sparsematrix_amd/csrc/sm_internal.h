@@ -46,6 +46,9 @@ struct XbandDev {
     float *d_val = nullptr;
     float *d_partials = nullptr;      // (n_slabs - 1) * n_rows slab partial sums (one SpMV in flight)
     int32_t *d_tickets = nullptr;     // 4 x n_blocks slab hand-off control words, zero between SpMVs
+    // band2 kind (band2.cpp): d_chunk_start = tile -> first band (n_tiles + 1), d_word =
+    // the lane-interleaved entries (4096 per band), d_band_clo = each band's first column.
+    int32_t *d_band_clo = nullptr;
 };
 
 struct Plan {
@@ -77,6 +80,9 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               const float *val, const float *x, float *y, float alpha,
                               float beta, float *partials, hipStream_t s);
 hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
+                             float *y, float alpha, float beta, hipStream_t s);
+// Balanced-band kind (kernels_band2.hip).
+hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
 // xp[i] = x[perm[i]], i < n.
 hipError_t launch_x_relabel(int64_t n, const int32_t *perm, const float *x, float *xp,

@@ -28,7 +28,7 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
 //             column order so the x gathers of one wave-instruction hit a few cache
 //             lines; LDS holds only the accumulators (measured slower, kept for A/B).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3 };
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
@@ -59,5 +59,41 @@ struct XbandHost {
 bool xband_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, XbBits bits, int waves, XbandHost &out, bool col_order = false,
                  int32_t start_rows = 0);
+
+}  // namespace smamd
+
+namespace smamd {
+
+// ---------------------------------------------------------------------------
+// "band2" layout (kernels_band2.hip): balanced bands.
+// Tiles = (block of <= 16384 rows, slab of columns), as the blocked kind, but a
+// tile's bands are variable column windows [clo, chi) of at most kB2Window columns
+// holding at most kB2Chunks chunks of 64 entries -- the builder closes a band when
+// either fills -- so every wave applies exactly two chunks per band and a band's
+// entries are one 16-byte load per lane.  Entry word: column - clo (14 bits) |
+// rank in the row's segment (4 bits, all ones = dummy) | row in block (14 bits),
+// stored XOR the dummy word.  Storage per band: 4096 uint32, lane-interleaved
+// [wave][lane][word of chunk 2w, word of chunk 2w+1, value bits of 2w, of 2w+1].
+constexpr int kB2ColBits = 14, kB2RankBits = 4, kB2RowBits = 14;
+constexpr int kB2Window = 8192;          // columns of x staged per band (32 KiB)
+constexpr int kB2Chunks = 32;            // 16 waves x 2 chunks
+constexpr int kB2BlockRows = 1 << kB2RowBits;
+constexpr uint32_t kB2DummyRank = (1u << kB2RankBits) - 1u;
+constexpr uint32_t kB2DummyWord = kB2DummyRank << kB2ColBits;
+
+struct Band2Host {
+    int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
+    int32_t max_bands_per_tile = 0;
+    int64_t n_bands = 0;                 // over all tiles
+    std::vector<int32_t> tile_band_start;   // n_blocks * n_slabs + 1 (tile t = b * S + s)
+    std::vector<int32_t> band_clo;          // first column of each band's window (multiple of 4)
+    std::vector<uint32_t> ent;              // 4096 per band
+    int64_t real_terms = 0;                 // for the padding report
+};
+
+// Returns false when the layout does not apply: a row segment longer than 14
+// terms inside one band window, unsorted columns, or size limits.
+bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out);
 
 }  // namespace smamd

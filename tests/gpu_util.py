@@ -73,3 +73,44 @@ def skewed_csr(n_rows: int, n_cols: int, lengths: np.ndarray, seed: int):
         col[rp[r]:rp[r + 1]] = np.sort(rng.integers(0, n_cols, int(lengths[r])))
     val = rng.uniform(-1, 1, nnz).astype(np.float32)
     return rp.astype(np.int32), col, val
+
+
+def with_env(key: str, value: str, fn):
+    """Run fn() with os.environ[key] = value (restored afterwards)."""
+    import os
+    old = os.environ.get(key)
+    os.environ[key] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(key, None)
+        else:
+            os.environ[key] = old
+
+
+def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int):
+    """The multi-slab band layouts' sum, restated on the oracle: each column slab
+    [s*slab_cols, (s+1)*slab_cols) summed in the reference's order (oracle.csr_spmv)
+    -- slab 0 from beta*y, later slabs from -0.0 -- then the slab sums added in slab
+    order in fp32.  Bit-exact target for has_xband 2/3/4 with several slabs."""
+    import oracle
+    rp = np.asarray(rp, np.int64)
+    ci = np.asarray(ci)
+    va = np.asarray(va, np.float32)
+    n = rp.size - 1
+    n_cols = x.size
+    n_slabs = max(1, -(-n_cols // slab_cols))
+    out = None
+    for s in range(n_slabs):
+        mask = (ci >= s * slab_cols) & (ci < (s + 1) * slab_cols)
+        cm = np.concatenate([[0], np.cumsum(mask)])
+        rps = np.zeros(n + 1, np.int64)
+        rps[1:] = cm[rp[1:]] - cm[rp[:-1]]
+        rps = np.cumsum(rps)
+        if s == 0:
+            p = oracle.csr_spmv(rps, ci[mask], va[mask], x, y0, alpha, beta)
+        else:
+            p = oracle.csr_spmv(rps, ci[mask], va[mask], x, np.full(n, -0.0, np.float32), alpha, 1.0)
+        out = p if out is None else (out + p).astype(np.float32)
+    return out

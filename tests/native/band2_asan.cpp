@@ -1,0 +1,134 @@
+// Host-only check of the balanced-band builder (sparsematrix_amd/csrc/band2.cpp),
+// built with AddressSanitizer by tests/test_xband_builder.py.  For several shapes
+// and slab counts: every term appears exactly once, each row's terms come out in
+// ascending column order across the tile's bands (bands ascend, ranks ascend in a
+// band), ranks are the term's index in its segment, a segment never spans two
+// chunks, columns stay inside the band's 8192-column window, bands ascend and never
+// overlap, and padding decodes as dummies with value 0.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "xband.h"
+
+using namespace smamd;
+
+static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
+                        const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
+                        bool expect_ok) {
+    Band2Host h;
+    const bool ok = band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h);
+    if (ok != expect_ok) { printf("FAIL build=%d expected %d\n", ok, expect_ok); return 1; }
+    if (!ok) return 0;
+    if ((int64_t)h.band_clo.size() != h.n_bands || (int64_t)h.ent.size() != h.n_bands * 4096) {
+        printf("FAIL sizes\n"); return 1; }
+    std::vector<std::vector<std::pair<int32_t, float>>> got(n_rows);
+    int64_t terms = 0;
+    for (int64_t t = 0; t < (int64_t)h.n_blocks * h.n_slabs; t++) {
+        const int64_t b = t / h.n_slabs, s = t % h.n_slabs;
+        const int64_t c0 = s * h.slab_cols, c1 = std::min<int64_t>(n_cols, c0 + h.slab_cols);
+        int64_t prev_hi = c0;
+        for (int64_t g = h.tile_band_start[t]; g < h.tile_band_start[t + 1]; g++) {
+            const int64_t clo = h.band_clo[g];
+            if (clo % 4) { printf("FAIL clo alignment\n"); return 1; }
+            int64_t lo_col = INT64_MAX, hi_col = -1;
+            for (int c = 0; c < kB2Chunks; c++) {
+                const int wave = c >> 1, k = c & 1;
+                std::vector<int> rows_seen;
+                for (int l = 0; l < 64; l++) {
+                    const uint32_t *e = &h.ent[(size_t)g * 4096 + (size_t)(wave * 64 + l) * 4];
+                    const uint32_t w = e[k] ^ kB2DummyWord;
+                    const uint32_t rank = (w >> kB2ColBits) & kB2DummyRank;
+                    float v;
+                    memcpy(&v, &e[2 + k], 4);
+                    if (rank == kB2DummyRank) {
+                        if (v != 0.0f || (w & ((1u << kB2ColBits) - 1u)) != 0) {
+                            printf("FAIL dummy\n"); return 1; }
+                        continue;
+                    }
+                    const uint32_t rl = w >> (kB2ColBits + kB2RankBits);
+                    const int64_t r = b * h.block_rows + rl;
+                    const int64_t cc = clo + (w & ((1u << kB2ColBits) - 1u));
+                    if (r >= n_rows || (int64_t)rl >= h.block_rows) { printf("FAIL row\n"); return 1; }
+                    if (cc - clo >= kB2Window || cc < c0 || cc >= c1) { printf("FAIL window\n"); return 1; }
+                    if ((int)rank != (int)std::count(rows_seen.begin(), rows_seen.end(), (int)rl)) {
+                        printf("FAIL rank\n"); return 1; }
+                    if (rank > 0 && (l == 0 || ((h.ent[(size_t)g * 4096 + (size_t)(wave * 64 + l - 1) * 4 + k] ^
+                                                 kB2DummyWord) >> (kB2ColBits + kB2RankBits)) != rl)) {
+                        printf("FAIL segment not on consecutive lanes\n"); return 1; }
+                    rows_seen.push_back((int)rl);
+                    got[r].push_back({(int32_t)cc, v});
+                    lo_col = std::min(lo_col, cc);
+                    hi_col = std::max(hi_col, cc);
+                    terms++;
+                }
+            }
+            if (hi_col < 0) { printf("FAIL empty band\n"); return 1; }
+            if (lo_col < prev_hi) { printf("FAIL bands overlap\n"); return 1; }
+            prev_hi = hi_col + 1;
+        }
+    }
+    // A row's segment inside one band sits in one chunk: implied by consecutive lanes +
+    // per-chunk ranks starting at 0 (checked above); the order check covers the rest.
+    for (int64_t r = 0; r < n_rows; r++) {
+        if ((int64_t)got[r].size() != rp[r + 1] - rp[r]) { printf("FAIL count row %lld\n", (long long)r); return 1; }
+        // terms of a row arrive band by band; within the tile's walk the bands ascend,
+        // but tiles (slabs) were walked in order too, so plain ascending order is required
+        for (int32_t e = rp[r]; e < rp[r + 1]; e++)
+            if (got[r][e - rp[r]].first != col[e] || got[r][e - rp[r]].second != val[e]) {
+                printf("FAIL order row %lld\n", (long long)r); return 1; }
+    }
+    if (terms != h.real_terms) { printf("FAIL real_terms\n"); return 1; }
+    return 0;
+}
+
+static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned seed, int slabs,
+                        bool expect_ok) {
+    std::mt19937 rng(seed);
+    std::vector<int32_t> rp(n_rows + 1), col;
+    std::vector<float> val;
+    for (int64_t r = 0; r < n_rows; r++) {
+        std::vector<int32_t> c(per_row);
+        for (auto &v : c) v = (int32_t)(rng() % n_cols);
+        std::sort(c.begin(), c.end());
+        c.erase(std::unique(c.begin(), c.end()), c.end());
+        for (auto v : c) { col.push_back(v); val.push_back((float)(rng() % 1000) + 1.0f); }
+        rp[r + 1] = (int32_t)col.size();
+    }
+    return check_layout(rp, col, val, n_rows, n_cols, slabs, expect_ok);
+}
+
+int main() {
+    int bad = 0;
+    for (int slabs : {1, 4, 16}) {
+        bad += check_random(200003, 300001, 16, 1, slabs, true);
+        bad += check_random(9000, 70001, 40, 2, slabs, true);
+        bad += check_random(5000, 1000, 5, 4, slabs, true);
+        bad += check_random(70000, 1000003, 16, 7, slabs, true);
+        bad += check_random(1, 50000, 30, 8, slabs, true);
+    }
+    // Contiguous runs of 40 columns: bands are cut inside them (<= 14 terms per row).
+    {
+        const int64_t n_rows = 3000, n_cols = 7000, w = 40;
+        std::mt19937 rng(9);
+        std::vector<int32_t> rp(n_rows + 1), col;
+        std::vector<float> val;
+        for (int64_t r = 0; r < n_rows; r++) {
+            const int32_t s = (int32_t)(rng() % (n_cols - w));
+            for (int j = 0; j < w; j++) { col.push_back(s + j); val.push_back(1.0f + j); }
+            rp[r + 1] = (int32_t)col.size();
+        }
+        bad += check_layout(rp, col, val, n_rows, n_cols, 1, true);
+        bad += check_layout(rp, col, val, n_rows, n_cols, 5, true);
+    }
+    // Unsorted columns are rejected.
+    {
+        std::vector<int32_t> rp = {0, 3}, col = {5, 2, 9};
+        std::vector<float> val = {1, 2, 3};
+        bad += check_layout(rp, col, val, 1, 10, 1, false);
+    }
+    printf(bad ? "band2_asan: FAILED\n" : "band2_asan: ok\n");
+    return bad ? 1 : 0;
+}

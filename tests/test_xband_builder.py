@@ -23,3 +23,19 @@ def test_xband_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "xband_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_band2_builder_under_asan(tmp_path):
+    """Balanced-band builder (band2.cpp): every term once, per row in ascending column
+    order, segments on consecutive lanes with their ranks, band windows respected."""
+    exe = tmp_path / "band2_asan"
+    src = [os.path.join(ROOT, "tests", "native", "band2_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "band2.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "band2_asan: ok" in r.stdout
