@@ -65,12 +65,14 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2"}
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "exact": "spmv_xband_kernel (exact band layout)",
            "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)",
            "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)",
-           "band2": "spmv_band2_kernel (balanced bands, distributed slab combine)"}
+           "band2": "spmv_band2_kernel (balanced bands, distributed slab combine)",
+           "cband": "spmv_band2_kernel<CB> (balanced bands of 4-byte codebook words, "
+                    "distributed slab combine)"}
 
 
 def load_traffic(workload: str, layout: str):
@@ -247,7 +249,13 @@ def main():
     traffic = load_traffic(workload, layout) if world == 1 else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-            "traffic": traffic, "kernel": KERNELS[layout], "layout": layout,
+            "traffic": traffic,
+            # the HBM bytes the kernel really moves (PMC) over its measured time
+            "traffic_frac": (round(traffic / (kmean * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                             if traffic else None),
+            "traffic_source": (f"profiles/traffic_{workload}_{layout}.json (rocprofv3 PMC, "
+                               "FETCH_SIZE x calibration + WRITE_SIZE)" if traffic else None),
+            "kernel": KERNELS[layout], "layout": layout,
             "xband_slabs": info["xband_slabs"], "xband_block_rows": info["xband_block_rows"],
             "kernel_ms_mean": round(kmean, 5), "kernel_ms_median": round(kmed, 5),
             "alg_bytes_per_launch": bytes_rank}

@@ -16,7 +16,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsparsematrix_amd.so")
+# SM_LIB_PATH: development A/B of alternative builds of the same library (tools/).
+LIB_PATH = os.environ.get("SM_LIB_PATH") or os.path.join(_HERE, "libsparsematrix_amd.so")
 
 # sm_status
 SM_OK = 0

@@ -38,21 +38,38 @@ struct Seg {
 // kernel passes a running sum up the lanes), then each single term of row r goes
 // to lane r mod 32 or 32 + r mod 32 when free -- so the 32 lanes of each half
 // read and write their accumulators in 32 distinct LDS banks -- else the highest
-// free lane.
+// free lane.  cband (ids != nullptr): lane 0 is the header (the chunk's base row),
+// terms take lanes 1..63 and carry their id, row - base and a continuation flag
+// instead of value bits and rank.
 void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const int32_t *col,
-                const float *val, int32_t clo_al) {
+                const float *val, const uint8_t *ids, int32_t clo_al) {
     bool used[64] = {false};
-    int next = 0;
     const int wave = c >> 1, k = c & 1;
+    const bool cb = ids != nullptr;
+    const int32_t base = segs.empty() ? 0 : segs.front().rl;   // segments come in row order
+    int next = 0;
+    if (cb) {
+        const uint32_t h = ((uint32_t)base & ((1u << kCbColBits) - 1u)) | (kCbDummyId << kCbColBits) |
+                           ((((uint32_t)base >> kCbColBits) & kCbOffMask) << kCbOffShift);
+        band_ent[(size_t)(wave * 64) * 2 + k] = h ^ kCbDummyWord;
+        used[0] = true;
+        next = 1;
+    }
     auto put = [&](const Seg &g, int32_t j, int lane) {
-        uint32_t *e = band_ent + ((size_t)(wave * 64 + lane)) * 4;
-        const uint32_t cb = (uint32_t)(col[g.s + j] - clo_al);
-        e[k] = (cb | ((uint32_t)j << kB2ColBits) | ((uint32_t)g.rl << (kB2ColBits + kB2RankBits))) ^
-               kB2DummyWord;
-        float v = val[g.s + j];
-        uint32_t vb;
-        __builtin_memcpy(&vb, &v, 4);
-        e[2 + k] = vb;
+        const uint32_t cbits = (uint32_t)(col[g.s + j] - clo_al);
+        if (cb) {
+            const uint32_t w = cbits | ((uint32_t)ids[g.s + j] << kCbColBits) |
+                               ((uint32_t)(g.rl - base) << kCbOffShift) | ((j > 0 ? 1u : 0u) << kCbContBit);
+            band_ent[(size_t)(wave * 64 + lane) * 2 + k] = w ^ kCbDummyWord;
+        } else {
+            uint32_t *e = band_ent + ((size_t)(wave * 64 + lane)) * 4;
+            e[k] = (cbits | ((uint32_t)j << kB2ColBits) | ((uint32_t)g.rl << (kB2ColBits + kB2RankBits))) ^
+                   kB2DummyWord;
+            float v = val[g.s + j];
+            uint32_t vb;
+            __builtin_memcpy(&vb, &v, 4);
+            e[2 + k] = vb;
+        }
         used[lane] = true;
     };
     for (const Seg &g : segs)
@@ -68,9 +85,19 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
     }
 }
 
-void build_tile(const int32_t *rp, const int32_t *col, const float *val, int64_t r0, int64_t r1,
-                int64_t c0, int64_t c1, TileOut &out) {
+void build_tile(const int32_t *rp, const int32_t *col, const float *val, const uint8_t *ids,
+                int64_t r0, int64_t r1, int64_t c0, int64_t c1, TileOut &out) {
     const int64_t nr = r1 - r0;
+    const bool cb = ids != nullptr;
+    // Chunk capacity, longest segment and row span of one chunk.
+    const int cap = cb ? kCbChunkTerms : 64;
+    const int32_t max_seg = cb ? kCbChunkTerms : (int32_t)kB2DummyRank - 1;
+    const int32_t span = cb ? kCbRowSpan : INT32_MAX;
+    const size_t band_words = cb ? 2048 : 4096;
+    // A new chunk opens when the segment does not fit the current one (terms or rows).
+    auto opens = [&](int fill, int32_t base, const Seg &g) {
+        return fill + g.n > cap || g.rl - base >= span;
+    };
     std::vector<int32_t> cur((size_t)nr), end((size_t)nr);
     std::vector<int32_t> hist((size_t)(c1 - c0) + 1, 0);
     for (int64_t r = r0; r < r1; r++) {
@@ -100,20 +127,22 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, int64_t
         for (;;) {   // pack; shrink chi until the band fits
             segs.clear();
             bool retry = false;
-            int chunks = 0, fill = 64;
+            int chunks = 0, fill = cap;
+            int32_t base = 0;
             for (int64_t r = 0; r < nr && !retry; r++) {
                 const int32_t s = cur[(size_t)r];
                 int32_t n = 0;
                 while (s + n < end[(size_t)r] && col[s + n] < chi) n++;
                 if (n == 0) continue;
-                if (n > (int32_t)kB2DummyRank - 1) {   // ranks 0..13 + dummy 15: cut the band
-                    chi = col[s + kB2DummyRank - 1];
+                if (n > max_seg) {   // band2: ranks 0..13 + dummy 15; cband: one chunk
+                    chi = col[s + max_seg];
                     retry = true;
                     break;
                 }
-                if (fill + n > 64) { chunks++; fill = 0; }
+                const Seg g{(int32_t)r, s, n};
+                if (opens(fill, base, g)) { chunks++; fill = 0; base = g.rl; }
                 fill += n;
-                segs.push_back(Seg{(int32_t)r, s, n});
+                segs.push_back(g);
             }
             if (retry) continue;
             if (chunks > kB2Chunks) {
@@ -124,19 +153,20 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, int64_t
         }
         // Emit: segments into chunks in row order.
         const size_t base = out.ent.size();
-        out.ent.resize(base + 4096, 0u);   // dummies: word 0 (= dummy ^ dummy), value 0
+        out.ent.resize(base + band_words, 0u);   // dummies: word 0 (= dummy ^ dummy), value 0
         out.clo.push_back((int32_t)clo_al);
         chunk_segs.assign(kB2Chunks, {});
-        int c = -1, fill = 64;
+        int c = -1, fill = cap;
+        int32_t cbase = 0;
         for (const Seg &g : segs) {
-            if (fill + g.n > 64) { c++; fill = 0; }
+            if (opens(fill, cbase, g)) { c++; fill = 0; cbase = g.rl; }
             fill += g.n;
             chunk_segs[(size_t)c].push_back(g);
             cur[(size_t)g.rl] += g.n;
             out.terms += g.n;
         }
         for (int k = 0; k <= c; k++)
-            emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, (int32_t)clo_al);
+            emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al);
         clo = chi;
     }
     for (int64_t r = 0; r < nr; r++)
@@ -146,8 +176,10 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, int64_t
 }  // namespace
 
 bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t n_slabs, Band2Host &out) {
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids) {
     out = Band2Host();
+    out.codebook = ids != nullptr;
+    const int64_t band_words = ids ? 2048 : 4096;
     if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)
@@ -166,7 +198,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
         th.emplace_back([&, t] {
             for (int64_t i = t; i < ntile; i += nthr) {
                 const int64_t b = i / ns, s = i % ns;
-                build_tile(rp, col, val, b * br, std::min<int64_t>(n_rows, (b + 1) * br), s * sc,
+                build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), s * sc,
                            std::min<int64_t>(n_cols, (s + 1) * sc), tiles[(size_t)i]);
             }
         });
@@ -189,11 +221,35 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     if (nb * 4096 >= ((int64_t)1 << 31)) return false;   // 32-bit entry offsets (x 4 bytes per dword)
     out.n_bands = nb;
     out.band_clo.reserve((size_t)nb);
-    out.ent.reserve((size_t)nb * 4096);
+    out.ent.reserve((size_t)(nb * band_words));
     for (auto &t : tiles) {
         out.band_clo.insert(out.band_clo.end(), t.clo.begin(), t.clo.end());
         out.ent.insert(out.ent.end(), t.ent.begin(), t.ent.end());
         std::vector<uint32_t>().swap(t.ent);
+    }
+    return true;
+}
+
+bool codebook_ids(const float *val, int64_t n, std::vector<float> &table, std::vector<uint8_t> &ids) {
+    // Open-addressing set of at most 255 bit patterns (512 slots).
+    constexpr uint32_t kSlots = 512;
+    uint32_t key[kSlots];
+    int16_t id[kSlots];
+    for (uint32_t i = 0; i < kSlots; i++) id[i] = -1;
+    table.clear();
+    ids.assign((size_t)n, 0);
+    for (int64_t e = 0; e < n; e++) {
+        uint32_t b;
+        __builtin_memcpy(&b, &val[e], 4);
+        uint32_t h = (b * 2654435761u) >> 23;   // 9 bits
+        while (id[h] >= 0 && key[h] != b) h = (h + 1) & (kSlots - 1);
+        if (id[h] < 0) {
+            if (table.size() >= kCbDummyId) return false;
+            key[h] = b;
+            id[h] = (int16_t)table.size();
+            table.push_back(val[e]);
+        }
+        ids[(size_t)e] = (uint8_t)id[h];
     }
     return true;
 }

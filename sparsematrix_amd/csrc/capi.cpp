@@ -85,9 +85,15 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.xb.d_partials);
     (void)hipFree(m->plan.xb.d_tickets);
     (void)hipFree(m->plan.xb.d_band_clo);
+    (void)hipFree(m->plan.xb.d_table);
     (void)hipFree(m->plan.d_perm);
     (void)hipFree(m->plan.d_rcol);
     (void)hipFree(m->plan.d_xperm);
+    (void)hipFree(m->d_ws);
+    if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
+    m->d_ws = nullptr;
+    m->ws_bytes = 0;
+    m->ws_ready = nullptr;
     m->d_row_ptr = m->d_col = nullptr;
     m->d_val = nullptr;
     m->plan = Plan();
@@ -142,16 +148,18 @@ XbKind xband_kind_setting(const sm_matrix *m) {
     if (e && strcmp(e, "gather") == 0) return kXbGather;
     if (e && strcmp(e, "blocked") == 0) return kXbBlocked;
     if (e && strcmp(e, "band2") == 0) return kXbBand2;
-    // band2 (balanced bands) where its bands fill: it declines to the blocked kind
-    // when they would be mostly padding (upload_band2).
-    return m->n_cols > kGatherCols ? kXbGather : kXbBand2;
+    if (e && strcmp(e, "cband") == 0) return kXbCband;
+    // cband (balanced bands, codebook words) where the values form a codebook of
+    // <= 255 entries, else band2; either declines to the blocked kind when its bands
+    // would be mostly padding (upload_band2).
+    return m->n_cols > kGatherCols ? kXbGather : kXbCband;
 }
 
 // Sweeping x through LDS (or walking its bands) pays when the L2 -> LDS bytes of
 // one kind's row blocks stay within 20x the matrix stream.
 static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
-                          : kind == kXbBand2  ? kB2RowBits
+                          : kind == kXbBand2 || kind == kXbCband ? kB2RowBits
                           : kind == kXbGather ? kXbGatherRowsLog2
                                               : kXbBlockedRowsLog2;
     const int64_t nblk = (m->n_rows + (1 << rows_log2) - 1) >> rows_log2;
@@ -169,30 +177,44 @@ bool want_xband(const sm_matrix *m) {
 }
 
 // Balanced-band layout (band2.cpp, kernels_band2.hip): slabs so there are about
-// kXbTargetTiles tiles of <= 16K rows.
+// kXbTargetTiles tiles of <= 16K rows.  kind cband: 4-byte codebook words when the
+// values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
-                              const float *val) {
+                              const float *val, XbKind kind) {
     const int64_t br = std::min<int64_t>(kB2BlockRows, m->n_rows);
     const int64_t nblk = (m->n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
         1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
     if (const char *e = getenv("SM_BAND2_SLABS"))   // development / tests: force the slab count
         want = std::max(1, std::min(16, atoi(e)));
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    const bool cb = kind == kXbCband && codebook_ids(val, m->nnz, table, ids);
     Band2Host bh;
-    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh)) return SM_OK;
+    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh, cb ? ids.data() : nullptr))
+        return SM_OK;
+    std::vector<uint8_t>().swap(ids);
     // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
     // dummies (wide or very sparse matrices), the padding would cost more HBM bytes
     // than the layout saves -- decline unless forced (SM_XBAND_KIND=band2).
     const char *kind_env = getenv("SM_XBAND_KIND");
-    const bool forced = kind_env && strcmp(kind_env, "band2") == 0;
+    const bool forced = kind_env && (strcmp(kind_env, "band2") == 0 || strcmp(kind_env, "cband") == 0);
     if (!forced && bh.n_bands > 0 &&
         (double)bh.real_terms < 0.7 * (double)bh.n_bands * kB2Chunks * 64)
         return SM_OK;
+    const int64_t band_words = cb ? 2048 : 4096;
     XbandDev &d = m->plan.xb;
     const int64_t ntile = (int64_t)bh.n_blocks * bh.n_slabs;
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, bh.n_bands), m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, bh.n_bands * 4096), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, bh.n_bands * band_words), m->device_bytes));
+    if (cb) {
+        SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
+        if (!table.empty())
+            SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+        d.table_size = (int32_t)table.size();
+    }
     if (bh.n_slabs > 1) {
         const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(bh.n_slabs - 1) * ps, m->device_bytes));
@@ -204,10 +226,10 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     if (bh.n_bands > 0) {
         SM_TRY_HIP(hipMemcpy(d.d_band_clo, bh.band_clo.data(), (size_t)bh.n_bands * 4,
                              hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(d.d_word, bh.ent.data(), (size_t)bh.n_bands * 4096 * 4,
+        SM_TRY_HIP(hipMemcpy(d.d_word, bh.ent.data(), (size_t)(bh.n_bands * band_words) * 4,
                              hipMemcpyHostToDevice));
     }
-    d.kind = kXbBand2;
+    d.kind = cb ? kXbCband : kXbBand2;
     d.threads = 1024;
     d.block_rows = bh.block_rows;
     d.band_cols = kB2Window;
@@ -222,10 +244,11 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
-    if (kind == kXbBand2) {
-        const sm_status st = upload_band2(m, rp, col, val);
+    if (kind == kXbBand2 || kind == kXbCband) {
+        const sm_status st = upload_band2(m, rp, col, val, kind);
         const char *e = getenv("SM_XBAND_KIND");
-        if (st == SM_OK && m->plan.xb.n_blocks == 0 && !(e && strcmp(e, "band2") == 0))
+        if (st == SM_OK && m->plan.xb.n_blocks == 0 &&
+            !(e && (strcmp(e, "band2") == 0 || strcmp(e, "cband") == 0)))
             return upload_xband(m, rp, col, val, kXbBlocked);   // declined: blocked kind
         return st;
     }
@@ -763,7 +786,8 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->xband_block_rows = m->plan.xb.block_rows;
     info->xband_slab_cols =
         m->plan.xb.n_blocks == 0 ? 0
-        : m->plan.xb.kind == kXbBand2 ? m->plan.xb.slab_bands   // band2 keeps slab columns there
+        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
+            ? m->plan.xb.slab_bands   // band2 / cband keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
@@ -868,7 +892,7 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     case SM_ALGO_AUTO:
     case SM_ALGO_XBAND:
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
-            e = m->plan.xb.kind == kXbBand2
+            e = m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
                     ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                     : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
             break;
@@ -947,26 +971,32 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         // back), then C = Y^T.  Same terms in the same order as the in-place kernel
         // below (bit-identical); the matrix is streamed once instead of m times.
         const int64_t mp = (m + 3) & ~3;
-        // Workspace per call like the reference's temp buffer (sparse-matrix.cc:155-161),
-        // freed after the stream drains (the call returns with the product done).  A
-        // stream-ordered hipMallocAsync workspace gave wrong sums when driven from the C++
-        // harness (tools/blas_test.cc, legacy null stream), so it is not used.
-        float *ws = nullptr;
+        // The matrix's workspace (sm_internal.h), where the reference allocates a temp
+        // buffer per call (sparse-matrix.cc:155-161): stream-ordered behind the previous
+        // call's kernels, so back-to-back calls neither block the host nor share bytes.
         const size_t ws_bytes = (size_t)(k + n) * mp * sizeof(float);
-        e = hipMalloc((void **)&ws, ws_bytes);
-        float *X = ws, *Y = ws + k * mp;
+        std::lock_guard<std::mutex> lk(mat->ws_mu);
+        e = hipSuccess;
+        if (!mat->ws_ready) e = hipEventCreateWithFlags(&mat->ws_ready, hipEventDisableTiming);
+        else e = hipStreamWaitEvent(s, mat->ws_ready, 0);
+        if (e == hipSuccess && mat->ws_bytes < ws_bytes) {
+            // Grow: the old buffer is released once its last user has finished.
+            e = hipEventSynchronize(mat->ws_ready);
+            if (e == hipSuccess) e = hipFree(mat->d_ws);
+            mat->d_ws = nullptr;
+            mat->ws_bytes = 0;
+            if (e == hipSuccess) e = hipMalloc((void **)&mat->d_ws, ws_bytes);
+            if (e == hipSuccess) mat->ws_bytes = ws_bytes;
+            else mat->d_ws = nullptr;
+        }
+        float *X = mat->d_ws, *Y = mat->d_ws + k * mp;
         if (e == hipSuccess) e = launch_transpose(a, m, (int32_t)k, lda, X, mp, s);
         if (e == hipSuccess) e = launch_transpose(c, m, (int32_t)n, ldc, Y, mp, s);
         if (e == hipSuccess)
             e = launch_spmm_rowpanel((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val,
                                      (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, s);
         if (e == hipSuccess) e = launch_transpose(Y, (int32_t)n, m, mp, c, ldc, s);
-        if (ws) {
-            hipError_t ef = hipStreamSynchronize(s);
-            const hipError_t ef2 = hipFree(ws);
-            if (ef == hipSuccess) ef = ef2;
-            if (e == hipSuccess) e = ef;
-        }
+        if (e == hipSuccess) e = hipEventRecord(mat->ws_ready, s);
         e = after_launch(e, s, "sm_addmatmat");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat (row panels)");
     }

@@ -3,23 +3,25 @@
 // One workgroup (1024 threads, 16 waves) per tile = (block of <= 16384 rows, slab
 // of columns), one per CU.  A tile's bands are column windows of <= 8192 columns
 // holding exactly 32 chunks of 64 entries (dummies pad the last): wave w applies
-// chunks 2w and 2w+1 of every band, and gets both -- two words, two values -- with
-// one 16-byte load per lane.  LDS: two x windows (double-buffered) and the block's
-// accumulators.
+// chunks 2w and 2w+1 of every band and gets both with one load per lane -- band2:
+// 16 bytes (two words, two fp32 values); cband: 8 bytes (two codebook words, the
+// values looked up in an LDS copy of the <= 255-entry table scaled by alpha).
+// LDS: two x windows (double-buffered), the block's accumulators (cband: and the
+// table).
 //
-// Per band p, every wave (static register rings, the loop unrolled by 6):
-//   load x window p+6 into registers (two float4 per lane),
-//   store x window p+1 (loaded five bands ago) into the free LDS buffer,
+// Per band p, every wave (static register rings, the loop unrolled by 2):
+//   load x window p+2 into registers (two float4 per lane),
+//   store x window p+1 (loaded a band ago) into the free LDS buffer,
 //   apply band p: term = x_lds[col] * (v * alpha), the chunk's terms added to the
 //   LDS accumulators in rank rounds (a row's segment runs up consecutive lanes by
 //   DPP, its last lane writes; no two lanes touch one row in a round, no atomics),
-//   load the entries of band p+6 (into the registers band p's entries held),
+//   load the entries of band p+2 (into the registers band p's entries held),
 //   barrier.
-// Why x goes through registers rather than LDS-DMA: vmcnt retires in issue order,
-// so a wave that waits for an LDS-DMA issued this band also waits for every entry
-// load it issued before -- the entry prefetch would collapse to one band.  Loaded
-// into registers six bands ahead, the x windows are waited for only when they are
-// old, and five bands of entries (80 KiB per CU) stay in flight.
+// x goes through registers rather than LDS-DMA: vmcnt retires in issue order, so a
+// wave waiting for an LDS-DMA issued this band would also wait for every entry load
+// issued before it.  Two bands of lookahead suffice: 4, 6 and 8 measured slower
+// (config 2, band2: 38.2 / 39.8 / 41.5 / - us; cband 38.0 / 39.3 / 40.6 / 44.0 us),
+// and so did deeper entry-only or x-only lookaheads.
 //
 // Summation order: bands ascend in column, a row's terms inside a band ascend in
 // column (ranks), so inside a tile every row is summed in the reference's order
@@ -32,35 +34,70 @@
 #include "xband_dev.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace smamd {
 namespace {
 
 constexpr int kB2Threads = 1024;
+// Lookaheads (bands) of the x windows and of the entries; development builds
+// override them (tools/r2_ab.sh).
+#ifndef SM_CB_XAHEAD
+#define SM_CB_XAHEAD 2
+#endif
+#ifndef SM_CB_EAHEAD
+#define SM_CB_EAHEAD 2
+#endif
+#ifndef SM_B2_XAHEAD
+#define SM_B2_XAHEAD 2
+#endif
+#ifndef SM_B2_EAHEAD
+#define SM_B2_EAHEAD 2
+#endif
+#ifndef SM_ENT_AUX
+#define SM_ENT_AUX kAuxNt
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // ABL (development only, SM_BAND2_ABLATE; results wrong): 1 skips the apply,
 // 2 the x loads and stores, 4 the entry loads, 8 the slab hand-off (plain stores),
-// 16 the band loop.
-template <int ABL, int PRIO>
+// 16 the band loop; cband only: 32 the codebook lookup, 64 the rank rounds, 128
+// the x gather (lane-ordered LDS reads instead), 256 the x LDS stores.
+// CB: the cband encoding (xband.h): one 32-bit word per term, values from the
+// codebook `table` (<= 255 entries), scaled by alpha once into LDS.
+template <int ABL, int PRIO, bool CB>
 __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
-    const uint32_t *__restrict__ ent, const float *__restrict__ x, float *__restrict__ y,
-    float *__restrict__ partials, int32_t *__restrict__ ctl, float alpha, float beta) {
+    const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
+    const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
+    int32_t *__restrict__ ctl, float alpha, float beta) {
     constexpr int BROWS = kB2BlockRows;
     constexpr int W = kB2Window;
     constexpr uint32_t kColMask = (1u << kB2ColBits) - 1u;
     constexpr uint32_t kRankMask = (1u << kB2RankBits) - 1u;
-    // Rings: x window p+A and the entries of band p+A are loaded at band p into the
+    // Rings: x window p+AX and the entries of band p+AE are loaded at band p into the
     // slots band p just freed (the x of window p was stored a band ago; the entries
     // of band p are loaded after its apply has decoded them).  Waiting for window p+1
-    // (loaded A-1 bands ago) retires every older load, so A bands of entries stay in
-    // flight: A = 6 keeps ~80 KiB per CU on the way from HBM.
-    constexpr int A = 6;            // lookahead = ring size = loop unroll
+    // (loaded AX-1 bands ago) retires every older load.  Measured (config 2): a
+    // lookahead of 2 bands beats 6 (38.3 vs 40.6 us cband, 38.3 vs 41.5 band2) --
+    // the loads need no more cover, and more of them in flight only slow the rest.
+    constexpr int AX = CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
+    constexpr int AE = CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
+    constexpr int U = AX > AE ? AX : AE;   // loop unroll: both rings' roles static
+    static_assert(U % AX == 0 && U % AE == 0 && U % 2 == 0, "ring sizes divide the unroll");
     static_assert(W == 2 * 4 * kB2Threads, "two float4 of x per lane per band");
     __shared__ __attribute__((aligned(16))) float xs[2][W];
-    __shared__ __attribute__((aligned(16))) float yacc[BROWS + 64];   // + a scratch slot per lane
-    __shared__ int32_t s_word[4];
+    // band2: + a scratch slot per lane (dummy lanes write there); cband writes only
+    // live lanes and uses the 160 KiB to the last byte: its hand-off words live in
+    // the x buffers once the band loop is over.
+    __shared__ __attribute__((aligned(16))) float yacc[BROWS + (CB ? 0 : 64)];
+    __shared__ int32_t s_word_b2[CB ? 1 : 4];
+    // cband: fl(table[id] * alpha) (0 past the table) in 32 copies, entry id of copy c
+    // at 32 * id + c: lane l reads copy l % 32, so a 32-lane group's reads hit 32
+    // distinct banks whatever the ids.
+    constexpr int kTabCopies = 16;
+    __shared__ float tab[CB ? 256 * kTabCopies : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int32_t t = blockIdx.x;
@@ -72,7 +109,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t r0 = b * block_rows;
     const int32_t nr = min(block_rows, n_rows - r0);
     const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
-    const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * 4096, (uint64_t)nb * 16384);
+    constexpr uint32_t kBandBytes = CB ? 8192u : 16384u;   // entries of one band
+    const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * (kBandBytes / 4), (uint64_t)nb * kBandBytes);
     // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi), read
     // by readlane; the window advances by 64 bands when the x loads reach its hi half.
     const int32_t *clg = band_clo + g0;
@@ -107,18 +145,22 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     auto store_x = [&](int buf, const float4 *xr) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            if (ABL & 2)
+            if (ABL & (2 | 256))
                 asm volatile("" ::"v"(xr[k].x), "v"(xr[k].y), "v"(xr[k].z), "v"(xr[k].w));
             else
                 *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * kB2Threads)]) = xr[k];
         }
     };
-    // Entries of band q: {word 2w, word 2w+1, value 2w, value 2w+1} for this lane;
-    // past the tile: zeros = dummies.
-    auto load_e = [&](int32_t q) -> u32x4 {
-        const uint32_t off = 16384u * (uint32_t)q + 16u * (uint32_t)tid;
-        if (ABL & 4) return u32x4{0u, 0u, 0u, 0u};
-        return __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, kAuxNt);
+    // Entries of band q: band2 {word 2w, word 2w+1, value 2w, value 2w+1}, cband
+    // {word 2w, word 2w+1} for this lane; past the tile: zeros = dummies.
+    using EV = typename std::conditional<CB, u32x2, u32x4>::type;
+    auto load_e = [&](int32_t q) -> EV {
+        const uint32_t off = kBandBytes * (uint32_t)q + (kBandBytes / kB2Threads) * (uint32_t)tid;
+        if (ABL & 4) return EV{};
+        if constexpr (CB)
+            return __builtin_amdgcn_raw_buffer_load_b64(e_src, off, 0, SM_ENT_AUX);
+        else
+            return __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, SM_ENT_AUX);
     };
 
     auto shr1 = [](float v) {   // lane i <- lane i-1 (lane 0 never has rank >= 1)
@@ -127,7 +169,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     auto shl1 = [](uint32_t v) {   // lane i <- lane i+1; lane 63 <- the dummy rank
         return (uint32_t)__builtin_amdgcn_update_dpp((int)kB2DummyRank, (int)v, 0x130, 0xF, 0xF, false);
     };
-    auto apply = [&](const float *xb, u32x4 e) {
+    auto apply_b2 = [&](const float *xb, u32x4 e) {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
         const uint32_t wd[2] = {e.x ^ kB2DummyWord, e.y ^ kB2DummyWord};
         const float va[2] = {__uint_as_float(e.z), __uint_as_float(e.w)};
@@ -172,6 +214,69 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
 
+    // Lane select by an SGPR lane mask (v_cndmask_b32 with the mask as its condition):
+    // lane i takes b where bit i of m is set, else a.
+    auto sel = [](uint64_t m, float a, float b) -> float {
+        float r;
+        asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+        return r;
+    };
+    // cband: row = chunk base (lane 0's header) + offset.  A segment's running sum
+    // moves up one lane per round in lane (= column) order; the lanes a round updates
+    // are an SGPR mask: the continuations whose predecessor finished last round.
+    auto apply_cb = [&](const float *xb, u32x2 e) {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
+        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
+        float xv[2], yv[2], tv[2];
+        uint32_t rl[2];
+        uint64_t live[2], cont[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
+            const uint32_t base = (h & kColMask) | (((h >> kCbOffShift) & kCbOffMask) << kCbColBits);
+            const uint32_t id = (wd[k] >> kCbColBits) & kCbDummyId;
+            live[k] = __ballot(id != kCbDummyId);
+            cont[k] = __ballot((int32_t)wd[k] < 0);
+            rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
+            xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd[k] & kColMask)];
+            tv[k] = (ABL & 32) ? __uint_as_float(id) : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+            yv[k] = yacc[rl[k]];
+        }
+        // Materialise all six reads before any write (one LDS wait per band).
+        asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
+        float tm[2], acc[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            tm[k] = __fmul_rn(xv[k], tv[k]);
+            acc[k] = __fadd_rn(yv[k], tm[k]);
+        }
+        if constexpr (!(ABL & 64)) {
+            uint64_t R0 = cont[0] & ~(cont[0] << 1), R1 = cont[1] & ~(cont[1] << 1);
+            while (R0 | R1) {
+                acc[0] = sel(R0, acc[0], __fadd_rn(shr1(acc[0]), tm[0]));
+                acc[1] = sel(R1, acc[1], __fadd_rn(shr1(acc[1]), tm[1]));
+                R0 = cont[0] & (R0 << 1);
+                R1 = cont[1] & (R1 << 1);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
+            const uint64_t last = live[k] & ~(cont[k] >> 1);
+            if ((last >> lane) & 1) yacc[rl[k]] = acc[k];
+        }
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    };
+
+    if constexpr (CB) {
+        constexpr int kPer = 256 * kTabCopies / kB2Threads;   // copies written per thread
+        static_assert(kPer % 4 == 0 && kTabCopies % kPer == 0, "whole float4 of one entry");
+        const int id = tid / (kTabCopies / kPer);   // one entry per thread
+        const float v = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
+#pragma unroll
+        for (int j = 0; j < kPer; j += 4)
+            *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
+    }
     // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row
     // without terms in this slab keeps the sign of a zero y), all loads in flight.
     constexpr int kQ = BROWS / (4 * kB2Threads);
@@ -207,37 +312,41 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
 
-    // Rings with static roles: x window q in X[q % A], entries of band q in E[q % A].
-    // Prologue = virtual bands -A..-1 (their loads in the loop's order), so the loads
+    // Rings with static roles: x window q in X[q % AX], entries of band q in E[q % AE].
+    // Prologue = virtual bands -U..-1 (their loads in the loop's order), so the loads
     // pending at the loop header are in the order the loop's back edge leaves them.
-    float4 X[A][2];
-    u32x4 E[A];
+    float4 X[AX][2];
+    EV E[AE];
 #pragma unroll
-    for (int q = 0; q < A; ++q) {
-        load_x(q, X[q]);
-        E[q] = load_e(q);
+    for (int v = -U; v < 0; ++v) {
+        if (v + AX >= 0) load_x(v + AX, X[v + AX]);
+        if (v + AE >= 0) E[v + AE] = load_e(v + AE);
     }
     store_x(0, X[0]);
     __syncthreads();
 
-    // Whole groups of A bands (static ring indices, no branch around a load or a
+    // Whole groups of U bands (static ring indices, no branch around a load or a
     // ring register: either makes hipcc copy registers and drain vmcnt).  Steps past
     // the tile's last band see only dummy entries (their loads go past the
     // descriptors: no memory request) and skip the barrier -- a uniform branch; the
-    // dummies only write the scratch slots and the x buffers nobody reads any more.
-    const int32_t nbu = (ABL & 16) ? 0 : (nb + A - 1) / A * A;
-    for (int32_t p = 0; p < nbu; p += A) {
+    // dummies write nothing but the x buffers nobody reads any more (band2: and the
+    // scratch slots).
+    const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
+    for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
-        for (int u = 0; u < A; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
-            if (q + A >= cw + 64) advance();
-            load_x(q + A, X[u]);
-            store_x((u + 1) & 1, X[(u + 1) % A]);
-            if (ABL & 1)
-                asm volatile("" ::"v"(E[u].x), "v"(E[u].y), "v"(E[u].z), "v"(E[u].w));
-            else
-                apply(xs[u & 1], E[u]);
-            E[u] = load_e(q + A);
+            if (q + AX >= cw + 64) advance();
+            load_x(q + AX, X[u % AX]);
+            store_x((u + 1) & 1, X[(u + 1) % AX]);
+            if constexpr (ABL & 1) {
+                asm volatile("" ::"v"(E[u % AE].x), "v"(E[u % AE].y));
+            } else if constexpr (CB) {
+                apply_cb(xs[u & 1], E[u % AE]);
+            } else {
+                apply_b2(xs[u & 1], E[u % AE]);
+            }
+            E[u % AE] = load_e(q + AE);
             if (q < nb) __syncthreads();
         }
     }
@@ -252,6 +361,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         for (int32_t i = nv + tid; i < nr; i += kB2Threads) y[r0 + i] = yacc[i];
         return;
     }
+    int32_t *s_word = s_word_b2;
+    if constexpr (CB) {   // every wave is past its last x read
+        __syncthreads();
+        s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
+    }
     slab_handoff<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
                              nr, slab, n_slabs, y_vec);
 }
@@ -261,8 +375,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s) {
     if (xb.n_blocks <= 0) return hipSuccess;
-    if (xb.kind != kXbBand2 || xb.n_slabs < 1 || xb.block_rows > kB2BlockRows ||
+    const bool cb = xb.kind == kXbCband;
+    if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > kB2BlockRows ||
         !xb.d_chunk_start || !xb.d_band_clo || (xb.n_bands > 0 && !xb.d_word) ||
+        (cb && (!xb.d_table || xb.table_size < 0 || xb.table_size > (int32_t)kCbDummyId)) ||
         (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
         return hipErrorInvalidValue;
     static const int abl = [] {
@@ -274,23 +390,42 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         return e ? atoi(e) : 2;
     }();
     const dim3 grid((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), block(kB2Threads);
-#define SM_B2(A, P)                                                                            \
-    hipLaunchKernelGGL((spmv_band2_kernel<A, P>), grid, block, 0, s, n_rows, n_cols,          \
-                       xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, \
-                       y, xb.d_partials, xb.d_tickets, alpha, beta)
+#define SM_B2(A, P, C)                                                                         \
+    hipLaunchKernelGGL((spmv_band2_kernel<A, P, C>), grid, block, 0, s, n_rows, n_cols,       \
+                       xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,   \
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+    if (cb) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true); break;
+        case 1: SM_B2(1, 2, true); break;
+        case 2: SM_B2(2, 2, true); break;
+        case 4: SM_B2(4, 2, true); break;
+        case 8: SM_B2(8, 2, true); break;
+        case 32: SM_B2(32, 2, true); break;
+        case 64: SM_B2(64, 2, true); break;
+        case 96: SM_B2(96, 2, true); break;
+        case 128: SM_B2(128, 2, true); break;
+        case 256: SM_B2(256, 2, true); break;
+        case 384: SM_B2(384, 2, true); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (abl) {
     case 0:
-        if (prio == 0) SM_B2(0, 0); else SM_B2(0, 2);
+        if (prio == 0) SM_B2(0, 0, false); else SM_B2(0, 2, false);
         break;
-    case 1: SM_B2(1, 2); break;
-    case 2: SM_B2(2, 2); break;
-    case 3: SM_B2(3, 2); break;
-    case 4: SM_B2(4, 2); break;
-    case 7: SM_B2(7, 2); break;
-    case 8: SM_B2(8, 2); break;
-    case 15: SM_B2(15, 2); break;
-    case 16: SM_B2(16, 2); break;
-    case 31: SM_B2(31, 2); break;
+    case 1: SM_B2(1, 2, false); break;
+    case 2: SM_B2(2, 2, false); break;
+    case 3: SM_B2(3, 2, false); break;
+    case 4: SM_B2(4, 2, false); break;
+    case 5: SM_B2(5, 2, false); break;
+    case 6: SM_B2(6, 2, false); break;
+    case 7: SM_B2(7, 2, false); break;
+    case 8: SM_B2(8, 2, false); break;
+    case 15: SM_B2(15, 2, false); break;
+    case 16: SM_B2(16, 2, false); break;
+    case 31: SM_B2(31, 2, false); break;
     default: return hipErrorInvalidValue;
     }
 #undef SM_B2

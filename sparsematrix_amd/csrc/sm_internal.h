@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -49,6 +50,9 @@ struct XbandDev {
     // band2 kind (band2.cpp): d_chunk_start = tile -> first band (n_tiles + 1), d_word =
     // the lane-interleaved entries (4096 per band), d_band_clo = each band's first column.
     int32_t *d_band_clo = nullptr;
+    // cband kind: the codebook (table_size <= 255 floats) the entries' ids index.
+    float *d_table = nullptr;
+    int32_t table_size = 0;
 };
 
 struct Plan {
@@ -145,4 +149,12 @@ struct sm_matrix {
     std::vector<uint8_t> pos, val;
     std::vector<int32_t> panel_row_off, panel_col_off;
     std::vector<int64_t> panel_begin, panel_end;
+    // Workspace of the row-panel AddMatMat (sm_addmatmat, 2 <= m <= 128), kept across
+    // calls.  Each call makes its stream wait on ws_ready (recorded after the previous
+    // call's last kernel), so calls on any streams use it in turn; it grows (after its
+    // last user has drained) only when a call needs more.
+    mutable std::mutex ws_mu;
+    mutable float *d_ws = nullptr;
+    mutable size_t ws_bytes = 0;
+    mutable hipEvent_t ws_ready = nullptr;
 };

@@ -28,7 +28,7 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
 //             column order so the x gathers of one wave-instruction hit a few cache
 //             lines; LDS holds only the accumulators (measured slower, kept for A/B).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4 };
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
@@ -81,7 +81,28 @@ constexpr int kB2BlockRows = 1 << kB2RowBits;
 constexpr uint32_t kB2DummyRank = (1u << kB2RankBits) - 1u;
 constexpr uint32_t kB2DummyWord = kB2DummyRank << kB2ColBits;
 
+// "cband" variant (codebook balanced bands): the same tiles and bands, but every term
+// is one 32-bit word -- column - clo (13 bits) | codebook id (8 bits, 255 = dummy) |
+// row - chunk base (10 bits) | continuation (1 bit: the term continues the previous
+// lane's segment of the same row) -- for matrices whose values take at most 255 distinct
+// fp32 bit patterns (the reference's own format: uint8 ids into a table of <= 255
+// floats, sparse-matrix.h:46-52).  Lane 0 of every chunk is the chunk's header: a
+// dummy whose column and row fields hold the base row (rows of the chunk lie in
+// [base, base + 1024)); a chunk holds <= 63 terms.  A row's segment inside a band
+// is a run of consecutive lanes, all but the first flagged as continuations.  Storage per band: 2048 uint32,
+// lane-interleaved [wave][lane][word of chunk 2w, word of chunk 2w+1], each stored
+// XOR kCbDummyWord (zero = dummy).
+constexpr int kCbColBits = 13, kCbIdBits = 8, kCbOffBits = 10, kCbContBit = 31;
+constexpr uint32_t kCbDummyId = (1u << kCbIdBits) - 1u;
+constexpr uint32_t kCbDummyWord = kCbDummyId << kCbColBits;
+constexpr int kCbOffShift = kCbColBits + kCbIdBits;
+constexpr uint32_t kCbOffMask = (1u << kCbOffBits) - 1u;
+constexpr int kCbChunkTerms = 63;        // lane 0 is the header
+constexpr int kCbRowSpan = 1 << kCbOffBits;
+static_assert(kB2Window <= (1 << kCbColBits), "window column fits the column field");
+
 struct Band2Host {
+    bool codebook = false;               // cband encoding (ent: 2048 words per band)
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
     int32_t max_bands_per_tile = 0;
     int64_t n_bands = 0;                 // over all tiles
@@ -91,9 +112,14 @@ struct Band2Host {
     int64_t real_terms = 0;                 // for the padding report
 };
 
-// Returns false when the layout does not apply: a row segment longer than 14
-// terms inside one band window, unsorted columns, or size limits.
+// Returns false when the layout does not apply: unsorted columns or size limits
+// (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
+// ids != nullptr builds the cband encoding: ids[e] = codebook id (< 255) of term e.
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t n_slabs, Band2Host &out);
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr);
+
+// Codebook of a value array: table[ids[e]] has the bits of val[e] for every e; false
+// when there are more than 255 distinct bit patterns (table then undefined).
+bool codebook_ids(const float *val, int64_t n, std::vector<float> &table, std::vector<uint8_t> &ids);
 
 }  // namespace smamd

@@ -56,7 +56,7 @@ def uniform_csr(n_rows: int, n_cols: int, per_row: int, seed: int, table=None):
         cols.sort(axis=1)
     if table is None:
         table = rng.uniform(-1, 1, 255).astype(np.float32)
-    val = table[rng.integers(0, 255, n_rows * per_row)].astype(np.float32)
+    val = table[rng.integers(0, len(table), n_rows * per_row)].astype(np.float32)
     rp = np.arange(0, n_rows * per_row + 1, per_row, dtype=np.int32)
     return rp, cols.reshape(-1).astype(np.int32), val
 

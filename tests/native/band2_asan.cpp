@@ -84,6 +84,72 @@ static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_
     return 0;
 }
 
+// cband encoding: rebuild every row from the 32-bit words (header base + offset,
+// codebook id, column), check segments sit on consecutive lanes, rows stay within
+// the chunk's 2048-row span, ids decode to the term's exact value bits.
+static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
+                           const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs) {
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    if (!codebook_ids(val.data(), (int64_t)val.size(), table, ids)) { printf("FAIL codebook\n"); return 1; }
+    for (size_t e = 0; e < val.size(); e++)
+        if (memcmp(&table[ids[e]], &val[e], 4) != 0) { printf("FAIL codebook id\n"); return 1; }
+    Band2Host h;
+    if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data())) {
+        printf("FAIL cband build\n"); return 1; }
+    if (!h.codebook || (int64_t)h.ent.size() != h.n_bands * 2048) { printf("FAIL cband sizes\n"); return 1; }
+    std::vector<std::vector<std::pair<int32_t, float>>> got(n_rows);
+    int64_t terms = 0;
+    for (int64_t t = 0; t < (int64_t)h.n_blocks * h.n_slabs; t++) {
+        const int64_t b = t / h.n_slabs, s = t % h.n_slabs;
+        const int64_t c0 = s * h.slab_cols, c1 = std::min<int64_t>(n_cols, c0 + h.slab_cols);
+        for (int64_t g = h.tile_band_start[t]; g < h.tile_band_start[t + 1]; g++) {
+            const int64_t clo = h.band_clo[g];
+            for (int c = 0; c < kB2Chunks; c++) {
+                const int wave = c >> 1, k = c & 1;
+                auto word = [&](int l) { return h.ent[(size_t)g * 2048 + (size_t)(wave * 64 + l) * 2 + k] ^ kCbDummyWord; };
+                const uint32_t hd = word(0);
+                if (((hd >> kCbColBits) & kCbDummyId) != kCbDummyId) { printf("FAIL header id\n"); return 1; }
+                const uint32_t base = (hd & ((1u << kCbColBits) - 1u)) | (((hd >> kCbOffShift) & kCbOffMask) << kCbColBits);
+                if (hd >> kCbContBit) { printf("FAIL header cont\n"); return 1; }
+                std::vector<int> rows_seen;
+                int prev_row = -1;
+                for (int l = 1; l < 64; l++) {
+                    const uint32_t w = word(l);
+                    const uint32_t id = (w >> kCbColBits) & kCbDummyId;
+                    if (id == kCbDummyId) {
+                        if (w != kCbDummyWord) { printf("FAIL cband dummy\n"); return 1; }
+                        prev_row = -1;
+                        continue;
+                    }
+                    if (id >= table.size()) { printf("FAIL id range\n"); return 1; }
+                    const uint32_t rl = base + ((w >> kCbOffShift) & kCbOffMask);
+                    const bool cont = (w >> kCbContBit) != 0;
+                    const int64_t r = b * h.block_rows + rl;
+                    const int64_t cc = clo + (w & ((1u << kCbColBits) - 1u));
+                    if (r >= n_rows || (int64_t)rl >= h.block_rows) { printf("FAIL cband row\n"); return 1; }
+                    if (cc - clo >= kB2Window || cc < c0 || cc >= c1) { printf("FAIL cband window\n"); return 1; }
+                    const int seen = (int)std::count(rows_seen.begin(), rows_seen.end(), (int)rl);
+                    if (seen > 0 && prev_row != (int)rl) { printf("FAIL cband segment lanes\n"); return 1; }
+                    if (cont != (seen > 0)) { printf("FAIL cband cont flag\n"); return 1; }
+                    rows_seen.push_back((int)rl);
+                    prev_row = (int)rl;
+                    got[r].push_back({(int32_t)cc, table[id]});
+                    terms++;
+                }
+            }
+        }
+    }
+    for (int64_t r = 0; r < n_rows; r++) {
+        if ((int64_t)got[r].size() != rp[r + 1] - rp[r]) { printf("FAIL cband count row %lld\n", (long long)r); return 1; }
+        for (int32_t e = rp[r]; e < rp[r + 1]; e++)
+            if (got[r][e - rp[r]].first != col[e] || memcmp(&got[r][e - rp[r]].second, &val[e], 4) != 0) {
+                printf("FAIL cband order row %lld\n", (long long)r); return 1; }
+    }
+    if (terms != h.real_terms) { printf("FAIL cband real_terms\n"); return 1; }
+    return 0;
+}
+
 static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned seed, int slabs,
                         bool expect_ok) {
     std::mt19937 rng(seed);
@@ -97,7 +163,15 @@ static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned se
         for (auto v : c) { col.push_back(v); val.push_back((float)(rng() % 1000) + 1.0f); }
         rp[r + 1] = (int32_t)col.size();
     }
-    return check_layout(rp, col, val, n_rows, n_cols, slabs, expect_ok);
+    int bad = check_layout(rp, col, val, n_rows, n_cols, slabs, expect_ok);
+    if (expect_ok) {   // the same pattern with a 255-value codebook (incl. -0.0 and +0.0)
+        for (size_t e = 0; e < val.size(); e++) {
+            const uint32_t i = rng() % 255;
+            val[e] = i == 0 ? -0.0f : (float)i * 0.37f - 40.0f;
+        }
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs);
+    }
+    return bad;
 }
 
 int main() {
@@ -122,6 +196,41 @@ int main() {
         }
         bad += check_layout(rp, col, val, n_rows, n_cols, 1, true);
         bad += check_layout(rp, col, val, n_rows, n_cols, 5, true);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, 1);   // 40-term segments fit a chunk
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, 5);
+    }
+    // Rows of 70 consecutive columns: cband cuts bands inside them (<= 63 terms).
+    {
+        const int64_t n_rows = 500, n_cols = 5000, w = 70;
+        std::mt19937 rng(10);
+        std::vector<int32_t> rp(n_rows + 1), col;
+        std::vector<float> val;
+        for (int64_t r = 0; r < n_rows; r++) {
+            const int32_t s = (int32_t)(rng() % (n_cols - w));
+            for (int j = 0; j < w; j++) { col.push_back(s + j); val.push_back((float)(j % 7)); }
+            rp[r + 1] = (int32_t)col.size();
+        }
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, 1);
+    }
+    // Sparse rows far apart: chunks close at the 2048-row span.
+    {
+        const int64_t n_rows = 16384, n_cols = 9000;
+        std::vector<int32_t> rp(n_rows + 1, 0), col;
+        std::vector<float> val;
+        for (int64_t r = 0; r < n_rows; r++) {
+            if (r % 3000 == 0) { col.push_back((int32_t)(r % n_cols)); val.push_back(2.0f); }
+            rp[r + 1] = (int32_t)col.size();
+        }
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, 1);
+    }
+    // More than 255 distinct values: no codebook.
+    {
+        std::vector<float> v(1000), table;
+        std::vector<uint8_t> ids;
+        for (int i = 0; i < 1000; i++) v[i] = (float)(i % 256);
+        if (codebook_ids(v.data(), 1000, table, ids)) { printf("FAIL codebook accepted 256 values\n"); bad++; }
+        for (int i = 0; i < 1000; i++) v[i] = (float)(i % 255);
+        if (!codebook_ids(v.data(), 1000, table, ids) || table.size() != 255) { printf("FAIL codebook 255\n"); bad++; }
     }
     // Unsorted columns are rejected.
     {

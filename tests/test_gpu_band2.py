@@ -1,4 +1,5 @@
-"""Balanced-band SpMV (has_xband == 4: band2.cpp + kernels_band2.hip) through the C ABI.
+"""Balanced-band SpMV through the C ABI: band2 (has_xband == 4, 8-byte entries) and
+cband (has_xband == 5, 4-byte codebook words), band2.cpp + kernels_band2.hip.
 
 Bit-exact targets: with one slab, the reference's order (oracle.csr_spmv); with
 several, the slab-order restatement (gpu_util.slab_order_spmv: every slab in the
@@ -24,13 +25,23 @@ def sm():
     return sparsematrix_amd
 
 
-def _band2(sm, rp, ci, va, n_cols, slabs=None):
+KINDS = {"band2": 4, "cband": 5}
+
+
+def _codebook(va, n=200, seed=0):
+    """The values requantised onto an n-entry table (cband needs <= 255 distinct)."""
+    table = np.random.default_rng(seed).uniform(-1, 1, n).astype(np.float32)
+    ids = np.random.default_rng(seed + 1).integers(0, n, va.size)
+    return table[ids].astype(np.float32)
+
+
+def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2"):
     def make():
-        return with_env("SM_XBAND_KIND", "band2", lambda: with_env(
+        return with_env("SM_XBAND_KIND", kind, lambda: with_env(
             "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
     M = with_env("SM_BAND2_SLABS", str(slabs), make) if slabs else make()
     info = M.info()
-    assert info["has_xband"] == 4, info
+    assert info["has_xband"] == KINDS[kind], info
     return M, info
 
 
@@ -54,9 +65,10 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
-def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs):
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind):
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
-    M, info = _band2(sm, rp, ci, va, n_cols, slabs)
+    M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
     if slabs == 1:
         assert info["xband_slabs"] == 1
     rng = np.random.default_rng(5)
@@ -67,22 +79,27 @@ def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs):
         _check(M, info, rp, ci, va, x, y0, alpha, beta, algo)
 
 
-def test_band2_long_segments_cut(sm):
-    """Rows with 40 consecutive columns: a band holds at most 14 terms of one row, so
-    the builder cuts bands inside such runs; order and results stay exact."""
-    n_rows, n_cols, w = 6000, 7000, 40
+@pytest.mark.parametrize("kind,w", [("band2", 40), ("cband", 40), ("cband", 90)])
+def test_band2_long_segments_cut(sm, kind, w):
+    """Rows of w consecutive columns: a band holds at most 14 (band2) / 63 (cband)
+    terms of one row, so the builder cuts bands inside longer runs; cband's 40-term
+    segments stay whole and run 39 rounds of the lane-to-lane sum."""
+    n_rows, n_cols = 6000, 7000
     starts = np.random.default_rng(3).integers(0, n_cols - w, n_rows)
     ci = (starts[:, None] + np.arange(w)[None, :]).reshape(-1).astype(np.int32)
     rp = np.arange(0, n_rows * w + 1, w, dtype=np.int32)
     va = np.random.default_rng(4).uniform(-1, 1, ci.size).astype(np.float32)
+    if kind == "cband":
+        va = _codebook(va)
     for slabs in (1, None):
-        M, info = _band2(sm, rp, ci, va, n_cols, slabs)
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
         x = np.random.default_rng(6).uniform(-1, 1, n_cols).astype(np.float32)
         y0 = np.random.default_rng(7).uniform(-1, 1, n_rows).astype(np.float32)
         _check(M, info, rp, ci, va, x, y0, 1.0, 0.5)
 
 
-def test_band2_ragged_rows_and_empty_regions(sm):
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_ragged_rows_and_empty_regions(sm, kind):
     """Empty rows, one dense row, column ranges without terms (bands skip them)."""
     rng = np.random.default_rng(11)
     n_rows, n_cols = 40000, 600000
@@ -98,16 +115,20 @@ def test_band2_ragged_rows_and_empty_regions(sm):
     rp[1:] = np.cumsum([len(c) for c in rows])
     ci = np.concatenate(rows).astype(np.int32)
     va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    if kind == "cband":
+        va = _codebook(va)
     for slabs in (1, None):
-        M, info = _band2(sm, rp, ci, va, n_cols, slabs)
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
         x = rng.uniform(-1, 1, n_cols).astype(np.float32)
         y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
         _check(M, info, rp, ci, va, x, y0, 1.3, 0.7)
 
 
-def test_band2_special_values_and_signed_zeros(sm):
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_special_values_and_signed_zeros(sm, kind):
     n_rows, n_cols = 30000, 50000
-    rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77)
+    rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77,
+                             table=np.random.default_rng(1).uniform(-1, 1, 250).astype(np.float32))
     va = va.copy()
     va[::997] = np.inf
     va[5::1009] = np.nan
@@ -120,7 +141,7 @@ def test_band2_special_values_and_signed_zeros(sm):
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     y0[:300] = -0.0
     for slabs in (1, None):
-        M, info = _band2(sm, rp, ci, va, n_cols, slabs)
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
         for alpha, beta in ((1.0, 1.0), (0.5, 0.0), (2.0, 3.0)):
             y = to_dev(y0)
             M.spmv(to_dev(x), y, alpha, beta, algo="xband")
@@ -130,13 +151,14 @@ def test_band2_special_values_and_signed_zeros(sm):
             assert np.array_equal(bits(got), bits(want))
 
 
-def test_band2_repeated_launches_reset_handoff(sm):
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_repeated_launches_reset_handoff(sm, kind):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
     torch = torch_dev()
     n_rows, n_cols = 300000, 400000
     rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=21)
-    M, info = _band2(sm, rp, ci, va, n_cols)
+    M, info = _band2(sm, rp, ci, va, n_cols, kind=kind)
     assert info["xband_slabs"] > 1
     rng = np.random.default_rng(22)
     x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
@@ -153,24 +175,35 @@ def test_band2_repeated_launches_reset_handoff(sm):
 
 
 def test_band2_config2_equals_blocked(sm):
-    """BASELINE config 2 (2^20 x 2^20, 16 terms/row): band2 and the blocked kind use
-    the same 4 slabs of 262144 columns and sum each in the reference's order, so
-    their results are bit-identical; sampled rows match the slab-order oracle."""
+    """BASELINE config 2 (2^20 x 2^20, 16 terms/row): cband (AUTO), band2 and the
+    blocked kind use the same 4 slabs of 262144 columns and sum each in the
+    reference's order, so their results are bit-identical."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n)
     Mb2 = with_env("SM_XBAND_KIND", "band2", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n))
     Mbl = with_env("SM_XBAND_KIND", "blocked", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n))
-    i2, ib = Mb2.info(), Mbl.info()
-    assert i2["has_xband"] == 4 and ib["has_xband"] == 2
-    assert i2["xband_slabs"] == ib["xband_slabs"] == 4
-    assert i2["xband_slab_cols"] == ib["xband_slab_cols"] == 262144
+    ic, i2, ib = Mcb.info(), Mb2.info(), Mbl.info()
+    assert ic["has_xband"] == 5 and i2["has_xband"] == 4 and ib["has_xband"] == 2
+    assert ic["xband_slabs"] == i2["xband_slabs"] == ib["xband_slabs"] == 4
+    assert ic["xband_slab_cols"] == i2["xband_slab_cols"] == ib["xband_slab_cols"] == 262144
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
-    y2, yb = y0.clone(), y0.clone()
-    Mb2.spmv(x, y2, 1.0, 0.5)
-    Mbl.spmv(x, yb, 1.0, 0.5)
+    yc, y2, yb = y0.clone(), y0.clone(), y0.clone()
+    Mcb.spmv(x, yc, 1.3, 0.5)
+    Mb2.spmv(x, y2, 1.3, 0.5)
+    Mbl.spmv(x, yb, 1.3, 0.5)
     torch.cuda.synchronize()
     assert torch.equal(y2.view(torch.int32), yb.view(torch.int32))
+    assert torch.equal(yc.view(torch.int32), yb.view(torch.int32))
+
+
+def test_cband_falls_back_without_codebook(sm):
+    """More than 255 distinct values: AUTO builds band2 (8-byte entries) instead."""
+    rp, ci, va = uniform_csr(50000, 60000, 8, seed=5)
+    va = np.random.default_rng(6).uniform(-1, 1, va.size).astype(np.float32)
+    M = with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, 60000))
+    assert M.info()["has_xband"] == 4

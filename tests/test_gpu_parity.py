@@ -730,3 +730,40 @@ def test_wide_matrix_dense_rows_fall_back_to_blocked(sm):
     y = to_dev(y0)
     M.spmv(to_dev(x), y, 1.0, 0.5)
     assert_terms_close(to_host(y), want, absum)
+
+
+def test_addmatmat_workspace_back_to_back(sm):
+    """Device AddMatMat (2 <= m <= 128) reuses the matrix's workspace: calls queued
+    back to back on one stream (growing it in between) and calls on two streams at
+    once are each bit-identical to the reference order (oracle.csr_spmm on C^T)."""
+    torch = torch_dev()
+    n_rows, n_cols = 6000, 5000                   # B: S = B^T is 5000 x 6000
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=41)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    k, n = M.NumRows(), M.NumCols()
+    assert (k, n) == (n_cols, n_rows)
+    rng = np.random.default_rng(42)
+
+    def case(m):
+        A = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+        C = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+        want = oracle.csr_spmm(rp.astype(np.int64), ci, va, np.ascontiguousarray(A.T),
+                               np.ascontiguousarray(C.T), 1.3, 0.7).T
+        return A, C, np.ascontiguousarray(want)
+
+    cases = [case(m) for m in (8, 32, 16, 100, 8)]
+    dev = [(to_dev(A.reshape(-1)), to_dev(C.reshape(-1))) for A, C, _ in cases]
+    for (A, C, _), (a_d, c_d) in zip(cases, dev):    # one stream, no sync in between
+        M.AddMatMat(a_d, A.shape[0], k, c_d, n, 1.3, 0.7, algo="auto")
+    torch.cuda.synchronize()
+    for (A, C, want), (_, c_d) in zip(cases, dev):
+        assert bits_equal(to_host(c_d).reshape(A.shape[0], n), want), A.shape[0]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    dev = [(to_dev(A.reshape(-1)), to_dev(C.reshape(-1))) for A, C, _ in cases[:2]]
+    torch.cuda.synchronize()
+    for (A, _, _), (a_d, c_d), st in zip(cases[:2], dev, (s1, s2)):
+        with torch.cuda.stream(st):
+            M.AddMatMat(a_d, A.shape[0], k, c_d, n, 1.3, 0.7, algo="auto")
+    torch.cuda.synchronize()
+    for (A, _, want), (_, c_d) in zip(cases[:2], dev):
+        assert bits_equal(to_host(c_d).reshape(A.shape[0], n), want), A.shape[0]

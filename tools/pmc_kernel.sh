@@ -1,13 +1,13 @@
 #!/bin/bash
 # SQ/LDS counters for one SpMV algorithm on config 2 (one rocprofv3 pass per group,
-# --kernel-trace only).  Usage: ALGO=xband bash tools/pmc_kernel.sh
+# --kernel-trace only).  Usage: ALGO=xband bash tools/pmc_kernel.sh, or PMC_CMD=<command>
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/pmck
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-CMD="python3 $ROOT/tools/spmv_sweep.py --tiles 4096 --algos ${ALGO:-xband} --replicas 2 --rounds 1 --reps 4"
+CMD=${PMC_CMD:-"python3 $ROOT/tools/spmv_sweep.py --tiles 4096 --algos ${ALGO:-xband} --replicas 2 --rounds 1 --reps 4"}
 G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
 G2="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE"
 G3="SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_ANY"
