@@ -3,7 +3,7 @@
 //
 // Per tile (block b of rows, slab s of columns) the builder walks the slab's
 // columns left to right and closes a band [clo, chi) as soon as either
-//   * its window from clo rounded down to 4 columns would pass kB2Window columns,
+//   * its window from clo rounded down to 4 columns would pass geom.window columns,
 //   * its terms, packed row by row into 64-entry chunks without splitting a row's
 //     segment (the row's run of terms inside the band), would need more than
 //     kB2Chunks chunks, or
@@ -42,7 +42,7 @@ struct Seg {
 // terms take lanes 1..63 and carry their id, row - base and a continuation flag
 // instead of value bits and rank.
 void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const int32_t *col,
-                const float *val, const uint8_t *ids, int32_t clo_al) {
+                const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom) {
     bool used[64] = {false};
     const int wave = c >> 1, k = c & 1;
     const bool cb = ids != nullptr;
@@ -63,8 +63,8 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
             band_ent[(size_t)(wave * 64 + lane) * 2 + k] = w ^ kCbDummyWord;
         } else {
             uint32_t *e = band_ent + ((size_t)(wave * 64 + lane)) * 4;
-            e[k] = (cbits | ((uint32_t)j << kB2ColBits) | ((uint32_t)g.rl << (kB2ColBits + kB2RankBits))) ^
-                   kB2DummyWord;
+            e[k] = (cbits | ((uint32_t)j << geom.col_bits) | ((uint32_t)g.rl << (geom.col_bits + kB2RankBits))) ^
+                   geom.dummy_word();
             float v = val[g.s + j];
             uint32_t vb;
             __builtin_memcpy(&vb, &v, 4);
@@ -86,7 +86,7 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
 }
 
 void build_tile(const int32_t *rp, const int32_t *col, const float *val, const uint8_t *ids,
-                int64_t r0, int64_t r1, int64_t c0, int64_t c1, TileOut &out) {
+                int64_t r0, int64_t r1, int64_t c0, int64_t c1, B2Geom geom, TileOut &out) {
     const int64_t nr = r1 - r0;
     const bool cb = ids != nullptr;
     // Chunk capacity, longest segment and row span of one chunk.
@@ -116,7 +116,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
     while (clo < c1 && count(clo, c1) > 0) {
         while (hist[(size_t)(clo - c0)] == 0) clo++;   // no band starts on an empty column
         const int64_t clo_al = clo & ~(int64_t)3;
-        const int64_t lim = std::min<int64_t>(c1, clo_al + kB2Window);
+        const int64_t lim = std::min<int64_t>(c1, clo_al + geom.window);
         // Largest chi <= lim with at most 32 * 64 terms (binary search on H).
         int64_t lo = clo + 1, hi = lim;
         while (lo < hi) {
@@ -166,7 +166,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
             out.terms += g.n;
         }
         for (int k = 0; k <= c; k++)
-            emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al);
+            emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al, geom);
         clo = chi;
     }
     for (int64_t r = 0; r < nr; r++)
@@ -176,15 +176,20 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
 }  // namespace
 
 bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids) {
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids, B2Geom geom) {
     out = Band2Host();
     out.codebook = ids != nullptr;
+    out.geom = geom;
+    if (geom.window > (1 << geom.col_bits) || (ids && geom.window > (1 << kCbColBits)) ||
+        geom.block_rows > ((int64_t)1 << (32 - geom.col_bits - kB2RankBits)) ||
+        geom.block_rows > ((int64_t)1 << (kCbColBits + kCbOffBits)))
+        return false;
     const int64_t band_words = ids ? 2048 : 4096;
     if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)
             if (col[e] <= col[e - 1]) return false;
-    const int32_t br = (int32_t)std::min<int64_t>(kB2BlockRows, n_rows);
+    const int32_t br = (int32_t)std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
     // Slabs of whole 256-column pieces.
     const int64_t sc = ((n_cols + n_slabs - 1) / n_slabs + 255) & ~(int64_t)255;
@@ -199,7 +204,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
             for (int64_t i = t; i < ntile; i += nthr) {
                 const int64_t b = i / ns, s = i % ns;
                 build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), s * sc,
-                           std::min<int64_t>(n_cols, (s + 1) * sc), tiles[(size_t)i]);
+                           std::min<int64_t>(n_cols, (s + 1) * sc), geom, tiles[(size_t)i]);
             }
         });
     for (auto &x : th) x.join();

@@ -181,7 +181,11 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
-    const int64_t br = std::min<int64_t>(kB2BlockRows, m->n_rows);
+    // Geometry: SM_BAND_TALL=1 / 0 forces the tall / wide tiles (xband.h B2Geom).
+    const char *tall_env = getenv("SM_BAND_TALL");
+    const bool tall = tall_env && atoi(tall_env) == 1;
+    const B2Geom geom = !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
+    const int64_t br = std::min<int64_t>(geom.block_rows, m->n_rows);
     const int64_t nblk = (m->n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
         1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
@@ -191,7 +195,8 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     std::vector<uint8_t> ids;
     const bool cb = kind == kXbCband && codebook_ids(val, m->nnz, table, ids);
     Band2Host bh;
-    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh, cb ? ids.data() : nullptr))
+    const B2Geom g = !tall ? kB2Wide : cb ? kB2TallCb : kB2TallB2;
+    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh, cb ? ids.data() : nullptr, g))
         return SM_OK;
     std::vector<uint8_t>().swap(ids);
     // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
@@ -232,7 +237,7 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     d.kind = cb ? kXbCband : kXbBand2;
     d.threads = 1024;
     d.block_rows = bh.block_rows;
-    d.band_cols = kB2Window;
+    d.band_cols = g.window;
     d.n_bands = (int32_t)std::min<int64_t>(bh.n_bands, INT32_MAX);
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;

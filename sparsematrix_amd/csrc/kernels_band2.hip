@@ -54,6 +54,9 @@ constexpr int kB2Threads = 1024;
 #ifndef SM_B2_EAHEAD
 #define SM_B2_EAHEAD 2
 #endif
+#ifndef SM_X_AUX
+#define SM_X_AUX 0
+#endif
 #ifndef SM_ENT_AUX
 #define SM_ENT_AUX kAuxNt
 #endif
@@ -62,20 +65,30 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // ABL (development only, SM_BAND2_ABLATE; results wrong): 1 skips the apply,
 // 2 the x loads and stores, 4 the entry loads, 8 the slab hand-off (plain stores),
 // 16 the band loop; cband only: 32 the codebook lookup, 64 the rank rounds, 128
-// the x gather (lane-ordered LDS reads instead), 256 the x LDS stores.
+// the x gather (lane-ordered LDS reads instead), 256 the x LDS stores, 512 the
+// per-band barrier (racy).
 // CB: the cband encoding (xband.h): one 32-bit word per term, values from the
 // codebook `table` (<= 255 entries), scaled by alpha once into LDS.
-template <int ABL, int PRIO, bool CB>
+// TALL: the tall geometry (xband.h B2Geom): 32K-row blocks, 4096 (cband 3840)
+// column windows, one float4 of x per lane per band.
+template <int ABL, int PRIO, bool CB, bool TALL>
 __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta) {
-    constexpr int BROWS = kB2BlockRows;
-    constexpr int W = kB2Window;
-    constexpr uint32_t kColMask = (1u << kB2ColBits) - 1u;
+    constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : kB2Wide;
+    constexpr int BROWS = G.block_rows;
+    constexpr int W = G.window;
+    constexpr int XV = (W + 4 * kB2Threads - 1) / (4 * kB2Threads);   // float4 of x per lane
+    constexpr int kB2Col = G.col_bits;                                // band2 word fields
+    constexpr uint32_t kB2Dummy = G.dummy_word();
+    constexpr uint32_t kColMask = (1u << kB2Col) - 1u;
     constexpr uint32_t kRankMask = (1u << kB2RankBits) - 1u;
+    // Every LDS byte counts in the tall geometry: band2 keeps per-lane scratch slots
+    // for its dummy lanes' writes only in the wide one.
+    constexpr bool kScratch = !CB && !TALL;
     // Rings: x window p+AX and the entries of band p+AE are loaded at band p into the
     // slots band p just freed (the x of window p was stored a band ago; the entries
     // of band p are loaded after its apply has decoded them).  Waiting for window p+1
@@ -86,17 +99,18 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     constexpr int AE = CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
     constexpr int U = AX > AE ? AX : AE;   // loop unroll: both rings' roles static
     static_assert(U % AX == 0 && U % AE == 0 && U % 2 == 0, "ring sizes divide the unroll");
-    static_assert(W == 2 * 4 * kB2Threads, "two float4 of x per lane per band");
+    static_assert(W % 4 == 0 && XV * 4 * kB2Threads >= W, "float4 slots cover the window");
     __shared__ __attribute__((aligned(16))) float xs[2][W];
-    // band2: + a scratch slot per lane (dummy lanes write there); cband writes only
-    // live lanes and uses the 160 KiB to the last byte: its hand-off words live in
-    // the x buffers once the band loop is over.
-    __shared__ __attribute__((aligned(16))) float yacc[BROWS + (CB ? 0 : 64)];
-    __shared__ int32_t s_word_b2[CB ? 1 : 4];
-    // cband: fl(table[id] * alpha) (0 past the table) in 32 copies, entry id of copy c
-    // at 32 * id + c: lane l reads copy l % 32, so a 32-lane group's reads hit 32
-    // distinct banks whatever the ids.
-    constexpr int kTabCopies = 16;
+    // Wide band2: + a scratch slot per lane (dummy lanes write there).  The other
+    // kinds write only live lanes and use the LDS nearly to the last byte: their
+    // hand-off words live in the x buffers once the band loop is over.
+    __shared__ __attribute__((aligned(16))) float yacc[BROWS + (kScratch ? 64 : 0)];
+    __shared__ int32_t s_word_b2[kScratch ? 4 : 1];
+    // cband: fl(table[id] * alpha) (0 past the table) in kTabCopies copies, entry id
+    // of copy c at kTabCopies * id + c: lane l reads copy l % kTabCopies, so the
+    // reads of a 32-lane group spread over the banks whatever the ids (wide: 16
+    // copies; tall: one, no room for more).
+    constexpr int kTabCopies = TALL ? 1 : 16;
     __shared__ float tab[CB ? 256 * kTabCopies : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -129,26 +143,28 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         clo_hi = cw + 64 + lane < nb ? clg[cw + 64 + lane] : 0;
     };
 
-    // x window q: float4 slots tid and tid + 1024 of [clo_q, clo_q + 8192); windows
-    // past the tile read nothing (offset past the descriptor).
+    // x window q: float4 slots tid (+ 1024) of [clo_q, clo_q + W); windows past the
+    // tile and slots past W read nothing (offset past the descriptor).
     auto load_x = [&](int32_t q, float4 *xr) {
         const int32_t c = q < nb ? clo_at(q) : 0;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t off = q < nb ? 4u * (uint32_t)(c + 4 * (tid + k * kB2Threads)) : 0xFFFFFFF0u;
+        for (int k = 0; k < XV; ++k) {
+            const int32_t slot = 4 * (tid + k * kB2Threads);
+            const uint32_t off = q < nb && slot < W ? 4u * (uint32_t)(c + slot) : 0xFFFFFFF0u;
             u32x4 v = {off, off, off, off};
-            if (!(ABL & 2)) v = __builtin_amdgcn_raw_buffer_load_b128(x_src, off, 0, 0);
+            if (!(ABL & 2)) v = __builtin_amdgcn_raw_buffer_load_b128(x_src, off, 0, SM_X_AUX);
             xr[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                                 __uint_as_float(v.w));
         }
     };
     auto store_x = [&](int buf, const float4 *xr) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < XV; ++k) {
+            const int32_t slot = 4 * (tid + k * kB2Threads);
             if (ABL & (2 | 256))
                 asm volatile("" ::"v"(xr[k].x), "v"(xr[k].y), "v"(xr[k].z), "v"(xr[k].w));
-            else
-                *reinterpret_cast<float4 *>(&xs[buf][4 * (tid + k * kB2Threads)]) = xr[k];
+            else if (W % (4 * kB2Threads) == 0 || slot < W)
+                *reinterpret_cast<float4 *>(&xs[buf][slot]) = xr[k];
         }
     };
     // Entries of band q: band2 {word 2w, word 2w+1, value 2w, value 2w+1}, cband
@@ -169,9 +185,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     auto shl1 = [](uint32_t v) {   // lane i <- lane i+1; lane 63 <- the dummy rank
         return (uint32_t)__builtin_amdgcn_update_dpp((int)kB2DummyRank, (int)v, 0x130, 0xF, 0xF, false);
     };
+    (void)kB2Dummy;
     auto apply_b2 = [&](const float *xb, u32x4 e) {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        const uint32_t wd[2] = {e.x ^ kB2DummyWord, e.y ^ kB2DummyWord};
+        const uint32_t wd[2] = {e.x ^ kB2Dummy, e.y ^ kB2Dummy};
         const float va[2] = {__uint_as_float(e.z), __uint_as_float(e.w)};
         float xv[2], yv[2];
         uint32_t rk[2], rl[2];
@@ -179,9 +196,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         bool more = false;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            rk[k] = (wd[k] >> kB2ColBits) & kRankMask;
+            rk[k] = (wd[k] >> kB2Col) & kRankMask;
             live[k] = rk[k] != kB2DummyRank;
-            rl[k] = wd[k] >> (kB2ColBits + kB2RankBits);   // dummies decode to row 0, column 0
+            rl[k] = wd[k] >> (kB2Col + kB2RankBits);   // dummies decode to row 0, column 0
             xv[k] = xb[wd[k] & kColMask];
             yv[k] = yacc[rl[k]];
             more |= live[k] && rk[k] > 0;
@@ -207,9 +224,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {   // every lane writes: the segment's last to its row
+        for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
             const bool last = live[k] && shl1(rk[k]) != rk[k] + 1u;
-            yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];
+            if constexpr (kScratch)
+                yacc[last ? rl[k] : (uint32_t)(BROWS + lane)] = acc[k];   // every lane writes
+            else if (last)
+                yacc[rl[k]] = acc[k];
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
@@ -269,13 +289,17 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     };
 
     if constexpr (CB) {
-        constexpr int kPer = 256 * kTabCopies / kB2Threads;   // copies written per thread
-        static_assert(kPer % 4 == 0 && kTabCopies % kPer == 0, "whole float4 of one entry");
-        const int id = tid / (kTabCopies / kPer);   // one entry per thread
-        const float v = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
+        if constexpr (kTabCopies == 1) {
+            if (tid < 256) tab[tid] = tid < table_size ? __fmul_rn(table[tid], alpha) : 0.0f;
+        } else {
+            constexpr int kPer = 256 * kTabCopies / kB2Threads;   // copies written per thread
+            static_assert(kPer % 4 == 0 && kTabCopies % kPer == 0, "whole float4 of one entry");
+            const int id = tid / (kTabCopies / kPer);   // one entry per thread
+            const float v = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
 #pragma unroll
-        for (int j = 0; j < kPer; j += 4)
-            *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
+            for (int j = 0; j < kPer; j += 4)
+                *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
+        }
     }
     // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row
     // without terms in this slab keeps the sign of a zero y), all loads in flight.
@@ -315,7 +339,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // Rings with static roles: x window q in X[q % AX], entries of band q in E[q % AE].
     // Prologue = virtual bands -U..-1 (their loads in the loop's order), so the loads
     // pending at the loop header are in the order the loop's back edge leaves them.
-    float4 X[AX][2];
+    float4 X[AX][XV];
     EV E[AE];
 #pragma unroll
     for (int v = -U; v < 0; ++v) {
@@ -347,7 +371,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 apply_b2(xs[u & 1], E[u % AE]);
             }
             E[u % AE] = load_e(q + AE);
-            if (q < nb) __syncthreads();
+            if (!(ABL & 512) && q < nb) __syncthreads();
         }
     }
 
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         return;
     }
     int32_t *s_word = s_word_b2;
-    if constexpr (CB) {   // every wave is past its last x read
+    if constexpr (!kScratch) {   // every wave is past its last x read
         __syncthreads();
         s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
     }
@@ -376,8 +400,11 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
                              float *y, float alpha, float beta, hipStream_t s) {
     if (xb.n_blocks <= 0) return hipSuccess;
     const bool cb = xb.kind == kXbCband;
-    if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > kB2BlockRows ||
-        !xb.d_chunk_start || !xb.d_band_clo || (xb.n_bands > 0 && !xb.d_word) ||
+    const bool tall = xb.band_cols != kB2Wide.window;
+    const B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+    if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
+        xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
+        (xb.n_bands > 0 && !xb.d_word) ||
         (cb && (!xb.d_table || xb.table_size < 0 || xb.table_size > (int32_t)kCbDummyId)) ||
         (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
         return hipErrorInvalidValue;
@@ -390,42 +417,46 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         return e ? atoi(e) : 2;
     }();
     const dim3 grid((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), block(kB2Threads);
-#define SM_B2(A, P, C)                                                                         \
-    hipLaunchKernelGGL((spmv_band2_kernel<A, P, C>), grid, block, 0, s, n_rows, n_cols,       \
+#define SM_B2(A, P, C, T)                                                                      \
+    hipLaunchKernelGGL((spmv_band2_kernel<A, P, C, T>), grid, block, 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,   \
                        xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+    if (tall) {
+        if (abl == 8) {
+            if (cb) SM_B2(8, 2, true, true); else SM_B2(8, 2, false, true);
+            return hipGetLastError();
+        }
+        if (abl != 0) return hipErrorInvalidValue;
+        if (cb) SM_B2(0, 2, true, true); else SM_B2(0, 2, false, true);
+        return hipGetLastError();
+    }
     if (cb) {
         switch (abl) {
-        case 0: SM_B2(0, 2, true); break;
-        case 1: SM_B2(1, 2, true); break;
-        case 2: SM_B2(2, 2, true); break;
-        case 4: SM_B2(4, 2, true); break;
-        case 8: SM_B2(8, 2, true); break;
-        case 32: SM_B2(32, 2, true); break;
-        case 64: SM_B2(64, 2, true); break;
-        case 96: SM_B2(96, 2, true); break;
-        case 128: SM_B2(128, 2, true); break;
-        case 256: SM_B2(256, 2, true); break;
-        case 384: SM_B2(384, 2, true); break;
+        case 0: SM_B2(0, 2, true, false); break;
+        case 1: SM_B2(1, 2, true, false); break;
+        case 2: SM_B2(2, 2, true, false); break;
+        case 4: SM_B2(4, 2, true, false); break;
+        case 8: SM_B2(8, 2, true, false); break;
+        case 32: SM_B2(32, 2, true, false); break;
+        case 64: SM_B2(64, 2, true, false); break;
+        case 128: SM_B2(128, 2, true, false); break;
+        case 256: SM_B2(256, 2, true, false); break;
+        case 512: SM_B2(512, 2, true, false); break;
+        case 516: SM_B2(516, 2, true, false); break;
+        case 513: SM_B2(513, 2, true, false); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
     switch (abl) {
     case 0:
-        if (prio == 0) SM_B2(0, 0, false); else SM_B2(0, 2, false);
+        if (prio == 0) SM_B2(0, 0, false, false); else SM_B2(0, 2, false, false);
         break;
-    case 1: SM_B2(1, 2, false); break;
-    case 2: SM_B2(2, 2, false); break;
-    case 3: SM_B2(3, 2, false); break;
-    case 4: SM_B2(4, 2, false); break;
-    case 5: SM_B2(5, 2, false); break;
-    case 6: SM_B2(6, 2, false); break;
-    case 7: SM_B2(7, 2, false); break;
-    case 8: SM_B2(8, 2, false); break;
-    case 15: SM_B2(15, 2, false); break;
-    case 16: SM_B2(16, 2, false); break;
-    case 31: SM_B2(31, 2, false); break;
+    case 1: SM_B2(1, 2, false, false); break;
+    case 2: SM_B2(2, 2, false, false); break;
+    case 4: SM_B2(4, 2, false, false); break;
+    case 8: SM_B2(8, 2, false, false); break;
+    case 16: SM_B2(16, 2, false, false); break;
     default: return hipErrorInvalidValue;
     }
 #undef SM_B2

@@ -101,8 +101,22 @@ constexpr int kCbChunkTerms = 63;        // lane 0 is the header
 constexpr int kCbRowSpan = 1 << kCbOffBits;
 static_assert(kB2Window <= (1 << kCbColBits), "window column fits the column field");
 
+// Tile geometry.  wide: 16K-row blocks, 8192-column windows (the tile's block sums
+// in 64 KiB of LDS, two 32 KiB x windows); tall: 32K-row blocks (128 KiB of sums)
+// and 4096-column windows (cband: 3840, its table takes 1 KiB) -- half the x per
+// term of a tile, twice the slabs for the same tile count.  band2 word: column
+// (col_bits) | rank (4) | row (32 - col_bits - 4).
+struct B2Geom {
+    int32_t block_rows, window, col_bits;
+    constexpr uint32_t dummy_word() const { return kB2DummyRank << col_bits; }
+};
+constexpr B2Geom kB2Wide{1 << 14, 8192, 14};
+constexpr B2Geom kB2TallB2{1 << 15, 4096, 13};
+constexpr B2Geom kB2TallCb{1 << 15, 3840, 13};
+
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)
+    B2Geom geom = kB2Wide;
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
     int32_t max_bands_per_tile = 0;
     int64_t n_bands = 0;                 // over all tiles
@@ -116,7 +130,8 @@ struct Band2Host {
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
 // ids != nullptr builds the cband encoding: ids[e] = codebook id (< 255) of term e.
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr);
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
+                 B2Geom geom = kB2Wide);
 
 // Codebook of a value array: table[ids[e]] has the bits of val[e] for every e; false
 // when there are more than 255 distinct bit patterns (table then undefined).

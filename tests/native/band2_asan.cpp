@@ -17,9 +17,11 @@ using namespace smamd;
 
 static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
                         const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
-                        bool expect_ok) {
+                        bool expect_ok, B2Geom geom = kB2Wide) {
     Band2Host h;
-    const bool ok = band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h);
+    const bool ok = band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, nullptr, geom);
+    const uint32_t kDummy = geom.dummy_word();
+    const int kCol = geom.col_bits;
     if (ok != expect_ok) { printf("FAIL build=%d expected %d\n", ok, expect_ok); return 1; }
     if (!ok) return 0;
     if ((int64_t)h.band_clo.size() != h.n_bands || (int64_t)h.ent.size() != h.n_bands * 4096) {
@@ -39,24 +41,24 @@ static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_
                 std::vector<int> rows_seen;
                 for (int l = 0; l < 64; l++) {
                     const uint32_t *e = &h.ent[(size_t)g * 4096 + (size_t)(wave * 64 + l) * 4];
-                    const uint32_t w = e[k] ^ kB2DummyWord;
-                    const uint32_t rank = (w >> kB2ColBits) & kB2DummyRank;
+                    const uint32_t w = e[k] ^ kDummy;
+                    const uint32_t rank = (w >> kCol) & kB2DummyRank;
                     float v;
                     memcpy(&v, &e[2 + k], 4);
                     if (rank == kB2DummyRank) {
-                        if (v != 0.0f || (w & ((1u << kB2ColBits) - 1u)) != 0) {
+                        if (v != 0.0f || (w & ((1u << kCol) - 1u)) != 0) {
                             printf("FAIL dummy\n"); return 1; }
                         continue;
                     }
-                    const uint32_t rl = w >> (kB2ColBits + kB2RankBits);
+                    const uint32_t rl = w >> (kCol + kB2RankBits);
                     const int64_t r = b * h.block_rows + rl;
-                    const int64_t cc = clo + (w & ((1u << kB2ColBits) - 1u));
+                    const int64_t cc = clo + (w & ((1u << kCol) - 1u));
                     if (r >= n_rows || (int64_t)rl >= h.block_rows) { printf("FAIL row\n"); return 1; }
-                    if (cc - clo >= kB2Window || cc < c0 || cc >= c1) { printf("FAIL window\n"); return 1; }
+                    if (cc - clo >= geom.window || cc < c0 || cc >= c1) { printf("FAIL window\n"); return 1; }
                     if ((int)rank != (int)std::count(rows_seen.begin(), rows_seen.end(), (int)rl)) {
                         printf("FAIL rank\n"); return 1; }
                     if (rank > 0 && (l == 0 || ((h.ent[(size_t)g * 4096 + (size_t)(wave * 64 + l - 1) * 4 + k] ^
-                                                 kB2DummyWord) >> (kB2ColBits + kB2RankBits)) != rl)) {
+                                                 kDummy) >> (kCol + kB2RankBits)) != rl)) {
                         printf("FAIL segment not on consecutive lanes\n"); return 1; }
                     rows_seen.push_back((int)rl);
                     got[r].push_back({(int32_t)cc, v});
@@ -88,14 +90,15 @@ static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_
 // codebook id, column), check segments sit on consecutive lanes, rows stay within
 // the chunk's 2048-row span, ids decode to the term's exact value bits.
 static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
-                           const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs) {
+                           const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
+                           B2Geom geom = kB2Wide) {
     std::vector<float> table;
     std::vector<uint8_t> ids;
     if (!codebook_ids(val.data(), (int64_t)val.size(), table, ids)) { printf("FAIL codebook\n"); return 1; }
     for (size_t e = 0; e < val.size(); e++)
         if (memcmp(&table[ids[e]], &val[e], 4) != 0) { printf("FAIL codebook id\n"); return 1; }
     Band2Host h;
-    if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data())) {
+    if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data(), geom)) {
         printf("FAIL cband build\n"); return 1; }
     if (!h.codebook || (int64_t)h.ent.size() != h.n_bands * 2048) { printf("FAIL cband sizes\n"); return 1; }
     std::vector<std::vector<std::pair<int32_t, float>>> got(n_rows);
@@ -128,7 +131,7 @@ static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int
                     const int64_t r = b * h.block_rows + rl;
                     const int64_t cc = clo + (w & ((1u << kCbColBits) - 1u));
                     if (r >= n_rows || (int64_t)rl >= h.block_rows) { printf("FAIL cband row\n"); return 1; }
-                    if (cc - clo >= kB2Window || cc < c0 || cc >= c1) { printf("FAIL cband window\n"); return 1; }
+                    if (cc - clo >= geom.window || cc < c0 || cc >= c1) { printf("FAIL cband window\n"); return 1; }
                     const int seen = (int)std::count(rows_seen.begin(), rows_seen.end(), (int)rl);
                     if (seen > 0 && prev_row != (int)rl) { printf("FAIL cband segment lanes\n"); return 1; }
                     if (cont != (seen > 0)) { printf("FAIL cband cont flag\n"); return 1; }
@@ -164,12 +167,14 @@ static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned se
         rp[r + 1] = (int32_t)col.size();
     }
     int bad = check_layout(rp, col, val, n_rows, n_cols, slabs, expect_ok);
+    bad += check_layout(rp, col, val, n_rows, n_cols, slabs, expect_ok, kB2TallB2);
     if (expect_ok) {   // the same pattern with a 255-value codebook (incl. -0.0 and +0.0)
         for (size_t e = 0; e < val.size(); e++) {
             const uint32_t i = rng() % 255;
             val[e] = i == 0 ? -0.0f : (float)i * 0.37f - 40.0f;
         }
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2TallCb);
     }
     return bad;
 }

@@ -35,13 +35,15 @@ def _codebook(va, n=200, seed=0):
     return table[ids].astype(np.float32)
 
 
-def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2"):
+def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
     def make():
         return with_env("SM_XBAND_KIND", kind, lambda: with_env(
-            "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+            "SM_BAND_TALL", str(tall), lambda: with_env(
+                "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))))
     M = with_env("SM_BAND2_SLABS", str(slabs), make) if slabs else make()
     info = M.info()
     assert info["has_xband"] == KINDS[kind], info
+    assert info["xband_block_rows"] <= (32768 if tall else 16384), info
     return M, info
 
 
@@ -66,9 +68,10 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind):
+@pytest.mark.parametrize("tall", [0, 1])
+def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
-    M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
+    M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind, tall)
     if slabs == 1:
         assert info["xband_slabs"] == 1
     rng = np.random.default_rng(5)
@@ -125,7 +128,8 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-def test_band2_special_values_and_signed_zeros(sm, kind):
+@pytest.mark.parametrize("tall", [0, 1])
+def test_band2_special_values_and_signed_zeros(sm, kind, tall):
     n_rows, n_cols = 30000, 50000
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77,
                              table=np.random.default_rng(1).uniform(-1, 1, 250).astype(np.float32))
@@ -141,7 +145,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind):
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     y0[:300] = -0.0
     for slabs in (1, None):
-        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind, tall)
         for alpha, beta in ((1.0, 1.0), (0.5, 0.0), (2.0, 3.0)):
             y = to_dev(y0)
             M.spmv(to_dev(x), y, alpha, beta, algo="xband")
@@ -152,13 +156,14 @@ def test_band2_special_values_and_signed_zeros(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-def test_band2_repeated_launches_reset_handoff(sm, kind):
+@pytest.mark.parametrize("tall", [0, 1])
+def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
     torch = torch_dev()
     n_rows, n_cols = 300000, 400000
     rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=21)
-    M, info = _band2(sm, rp, ci, va, n_cols, kind=kind)
+    M, info = _band2(sm, rp, ci, va, n_cols, kind=kind, tall=tall)
     assert info["xband_slabs"] > 1
     rng = np.random.default_rng(22)
     x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
@@ -207,3 +212,27 @@ def test_cband_falls_back_without_codebook(sm):
     va = np.random.default_rng(6).uniform(-1, 1, va.size).astype(np.float32)
     M = with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, 60000))
     assert M.info()["has_xband"] == 4
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_tall_config2_vs_slab_oracle(sm, kind):
+    """BASELINE config 2 in the tall geometry (32K-row blocks, 8 slabs of 131072
+    columns): bit-identical to the 8-slab restatement of the reference order."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = with_env("SM_XBAND_KIND", kind, lambda: with_env(
+        "SM_BAND_TALL", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n)))
+    info = M.info()
+    assert info["has_xband"] == KINDS[kind] and info["xband_block_rows"] == 32768, info
+    assert info["xband_slabs"] == 8 and info["xband_slab_cols"] == 131072, info
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.3, 0.5)
+    torch.cuda.synchronize()
+    want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
+                           to_host(y0), 1.3, 0.5, 131072)
+    assert np.array_equal(bits(to_host(y)), bits(want))
