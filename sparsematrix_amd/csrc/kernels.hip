@@ -86,7 +86,9 @@ __global__ __launch_bounds__(256) void spmv_parity_kernel(int32_t n, const int32
 }
 
 // ---------------------------------------------------------------------------
-template <int THREADS, int TILE>
+// ABL (development only, SM_STREAM_ABLATE; results wrong): 1 replaces the x gathers
+// of short-row tiles by one broadcast address.
+template <int THREADS, int TILE, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
     const Tile *__restrict__ tiles, const Chunk *__restrict__ chunks, int32_t n_chunks,
     const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
@@ -178,8 +180,14 @@ __global__ __launch_bounds__(THREADS) void spmv_stream_kernel(
         float xg[kIt][4];
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
-            xg[it][0] = x[cc[it].x]; xg[it][1] = x[cc[it].y];
-            xg[it][2] = x[cc[it].z]; xg[it][3] = x[cc[it].w];
+            if constexpr (ABL & 1) {
+                const int32_t c0 = cc[it].x & 0;
+                xg[it][0] = x[c0]; xg[it][1] = x[c0 + (cc[it].y & 0)];
+                xg[it][2] = x[c0 + (cc[it].z & 0)]; xg[it][3] = x[c0 + (cc[it].w & 0)];
+            } else {
+                xg[it][0] = x[cc[it].x]; xg[it][1] = x[cc[it].y];
+                xg[it][2] = x[cc[it].z]; xg[it][3] = x[cc[it].w];
+            }
         }
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
@@ -509,11 +517,20 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               float beta, float *partials, hipStream_t s) {
     const int64_t grid = (int64_t)p.n_chunks + p.n_tiles;
     if (grid == 0) return hipSuccess;
+    static const int abl = [] {
+        const char *e = getenv("SM_STREAM_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
 #define SM_STREAM(TT)                                                                         \
     case TT:                                                                                  \
-        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)grid),     \
-                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp,  \
-                           col, val, x, y, alpha, beta, partials);                            \
+        if (abl == 1)                                                                         \
+            hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT, 1>), dim3((unsigned)grid), \
+                               dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
+                               col, val, x, y, alpha, beta, partials);                        \
+        else                                                                                  \
+            hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)grid), \
+                               dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
+                               col, val, x, y, alpha, beta, partials);                        \
         break;
     switch (p.tile_nnz) {
         SM_STREAM(1024) SM_STREAM(2048) SM_STREAM(4096) SM_STREAM(8192)
