@@ -65,13 +65,16 @@ typedef enum sm_status {
 typedef enum sm_trans { SM_NO_TRANS = 0, SM_TRANS = 1 } sm_trans;
 
 typedef enum sm_algo {
-    SM_ALGO_AUTO = 0,     /* band layout if built, else stream (SpMV); row-panel (SpMM) */
+    SM_ALGO_AUTO = 0,     /* band layout if built, else sell, else stream (SpMV); row-panel (SpMM) */
     SM_ALGO_PARITY = 1,   /* bit-exact with the reference for every row            */
     SM_ALGO_STREAM = 2,   /* nnz-balanced row tiles through LDS (+ long-row split) */
     SM_ALGO_VECTOR = 3,   /* L lanes per row (CSR-vector), shuffle reduction       */
-    SM_ALGO_XBAND = 4     /* x staged through LDS in column bands (the layout built at
-                             creation: exact or blocked, see sm_info.has_xband); falls
-                             back to STREAM when the matrix holds no band layout    */
+    SM_ALGO_XBAND = 4,    /* x staged through LDS in column bands (the layout built at
+                             creation, see sm_info.has_xband); falls back to SELL, then
+                             STREAM, when the matrix holds no band layout             */
+    SM_ALGO_SELL = 5      /* sorted sliced-ELL, one lane per row (every row up to the
+                             stream tile size bit-identical; longer rows as the stream
+                             plan's chunks); STREAM when the layout is not built       */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the
@@ -94,8 +97,9 @@ typedef struct sm_info {
     int32_t n_long_rows;        /* rows split across workgroups                */
     int32_t max_row_nnz;        /* longest row                                 */
     int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
-                                   2 blocked, 3 gather, 4 band2 (balanced bands);
-                                   2-4 sum each column slab in the reference's
+                                   2 blocked, 3 gather, 4 band2 (balanced bands),
+                                   5 cband (balanced bands, codebook words);
+                                   2-5 sum each column slab in the reference's
                                    order and add the slab sums in slab order     */
     int32_t xband_blocks, xband_bands;
     int32_t xband_slabs;        /* column slabs per row block (1: bit-identical) */
@@ -104,6 +108,7 @@ typedef struct sm_info {
     int32_t col_relabel;        /* 1: the stream SpMV gathers x through a column
                                    relabeling by descending degree (skewed graphs) */
     int32_t xband_slab_cols;    /* columns per slab (slab s = [s*c, (s+1)*c))   */
+    int64_t sell_slices;        /* sorted sliced-ELL slices of 64 rows (0: not built) */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */

@@ -31,7 +31,7 @@ SM_ERR_NO_DEVICE = 7
 
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
-ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4}
+ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
@@ -53,6 +53,7 @@ class SmInfo(C.Structure):
         ("max_row_nnz", C.c_int32), ("has_xband", C.c_int32), ("xband_blocks", C.c_int32),
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
+        ("sell_slices", C.c_int64),
     ]
 
 

@@ -16,6 +16,7 @@
 
 #include "encode.h"
 #include "sm_internal.h"
+#include "sell.h"
 #include "xband.h"
 
 using namespace smamd;
@@ -89,6 +90,12 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.d_perm);
     (void)hipFree(m->plan.d_rcol);
     (void)hipFree(m->plan.d_xperm);
+    (void)hipFree(m->plan.sell.d_off);
+    (void)hipFree(m->plan.sell.d_len);
+    (void)hipFree(m->plan.sell.d_row);
+    (void)hipFree(m->plan.sell.d_row_len);
+    (void)hipFree(m->plan.sell.d_col);
+    (void)hipFree(m->plan.sell.d_val);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
     m->d_ws = nullptr;
@@ -380,6 +387,50 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
     return SM_OK;
 }
 
+// Sorted sliced-ELL (sell.h, kernels_sell.hip) for the matrices no band layout
+// serves.  SM_SELL=0 / 1 disables / forces it; otherwise it is built for skewed
+// matrices -- those that get the column relabeling (power-law graphs, R-MAT).
+bool want_sell(const sm_matrix *m) {
+    const char *e = getenv("SM_SELL");
+    if (e && atoi(e) == 0) return false;
+    if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0) return false;
+    if (e && atoi(e) == 1) return true;
+    return m->plan.n_relabel > 0;
+}
+
+sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    Plan &p = m->plan;
+    std::vector<int32_t> rcol;
+    const int32_t *c = col;
+    if (p.n_relabel > 0) {   // the layout stores relabeled columns (x is permuted per SpMV)
+        rcol.resize((size_t)m->nnz);
+        SM_TRY_HIP(hipMemcpy(rcol.data(), p.d_rcol, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
+        c = rcol.data();
+    }
+    SellHost sh;
+    sell_build(rp, c, val, m->n_rows, p.tile_nnz, sh);   // longer rows: the plan's long rows
+    std::vector<int32_t>().swap(rcol);
+    if (sh.n_slices == 0) return SM_OK;
+    if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
+    SellDev &d = p.sell;
+    SM_TRY_HIP(dev_alloc(&d.d_off, sh.n_slices, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_len, sh.n_slices, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_row, sh.n_slices * kSellLanes, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_row_len, sh.n_slices * kSellLanes, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_col, sh.padded, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_val, sh.padded, m->device_bytes));
+    SM_TRY_HIP(hipMemcpy(d.d_off, sh.off.data(), sh.off.size() * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_len, sh.len.data(), sh.len.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_row, sh.row.data(), sh.row.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_row_len, sh.row_len.data(), sh.row_len.size() * 4, hipMemcpyHostToDevice));
+    if (sh.padded) {
+        SM_TRY_HIP(hipMemcpy(d.d_col, sh.col.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_val, sh.val.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
+    }
+    d.n_slices = sh.n_slices;
+    return SM_OK;
+}
+
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
     int32_t tile = tile_nnz_setting();
@@ -461,6 +512,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     sm_status st2 = upload_plan(m, rp);
     if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting(m));
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
+    if (st2 == SM_OK && want_sell(m)) st2 = upload_sell(m, rp, col, val);
     return st2;
 }
 
@@ -751,18 +803,21 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
     }
     st = upload_plan(m.get(), rp.data());
     const bool xband = want_xband(m.get());
-    if (st == SM_OK && (xband || want_relabel_size(m.get()))) {
+    const char *sell_env = getenv("SM_SELL");
+    const bool maybe_sell = !(sell_env && atoi(sell_env) == 0);
+    if (st == SM_OK && (xband || want_relabel_size(m.get()) || (sell_env && atoi(sell_env) == 1))) {
         std::vector<int32_t> ch((size_t)nnz);
         std::vector<float> vh((size_t)nnz);
         hipError_t e3 = hipSuccess;
         if (nnz) {
             e3 = hipMemcpy(ch.data(), m->d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost);
-            if (e3 == hipSuccess && xband)
+            if (e3 == hipSuccess && (xband || maybe_sell))
                 e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
         }
         st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR for band layout / relabeling");
         if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting(m.get()));
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
+        if (st == SM_OK && want_sell(m.get())) st = upload_sell(m.get(), rp.data(), ch.data(), vh.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }
     *out = m.release();
@@ -796,6 +851,7 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
+    info->sell_slices = m->plan.sell.n_slices;
     return SM_OK;
 }
 
@@ -902,8 +958,24 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
                     : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
             break;
         }
-        // fall through: no band layout (or unaligned x) -> stream kernel
+        // fall through: no band layout (or unaligned x) -> sell or stream kernel
         [[fallthrough]];
+    case SM_ALGO_SELL:
+        if (m->plan.sell.n_slices > 0) {
+            const float *xs = x;
+            const int32_t *lc = m->d_col;
+            if (m->plan.n_relabel > 0) {
+                e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
+                xs = m->plan.d_xperm;
+                lc = m->plan.d_rcol;
+            }
+            if (e == hipSuccess) e = launch_spmv_sell(m->plan.sell, xs, y, alpha, beta, s);
+            if (e == hipSuccess)
+                e = launch_spmv_long_rows(m->plan, m->d_row_ptr, lc, m->d_val, xs, y, alpha, beta,
+                                          m->plan.d_partials, s);
+            break;
+        }
+        [[fallthrough]];   // no sell layout -> stream kernel
     case SM_ALGO_STREAM:
         // Long-row partial sums (and the relabeled x) live in the matrix (allocated at
         // creation): SpMVs on one matrix must not run concurrently on different streams.
@@ -941,6 +1013,7 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     }
     const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
                         ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
+    if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND) algo = SM_ALGO_AUTO;   // SpMV layouts
     if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
         e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X,
                                  ldx, m->n_cols, Y, ldy, alpha, beta, s);

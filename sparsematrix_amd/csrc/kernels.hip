@@ -544,6 +544,29 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
     return hipGetLastError();
 }
 
+hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t *col,
+                                 const float *val, const float *x, float *y, float alpha,
+                                 float beta, float *partials, hipStream_t s) {
+    if (p.n_chunks == 0) return hipSuccess;
+    // Blocks [0, n_chunks) of the stream kernel are the long-row chunks; no tile runs.
+#define SM_LONG(TT)                                                                           \
+    case TT:                                                                                  \
+        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)p.n_chunks), \
+                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp,  \
+                           col, val, x, y, alpha, beta, partials);                            \
+        break;
+    switch (p.tile_nnz) {
+        SM_LONG(1024) SM_LONG(2048) SM_LONG(4096) SM_LONG(8192)
+        default: return hipErrorInvalidValue;
+    }
+#undef SM_LONG
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.n_long)), dim3(256), 0, s,
+                       p.n_long, p.d_long_rows, p.d_long_ptr, partials, y, beta);
+    return hipGetLastError();
+}
+
 hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
                               const float *val, const float *x, float *y, float alpha, float beta,
                               hipStream_t s) {

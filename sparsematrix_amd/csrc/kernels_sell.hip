@@ -1,0 +1,72 @@
+// kernels_sell.hip -- SpMV over the sorted sliced-ELL layout (sell.h, sell.cpp).
+//
+// One wavefront per slice of 64 rows, four slices per 256-thread workgroup, no LDS
+// and no barrier: lane l owns row row[s*64 + l] and walks term slots j = 0, 1, ...
+// of its slice; slot j of the 64 lanes is one coalesced 256-byte load of columns and
+// one of values, then 64 x gathers.  Each lane adds x * (v * alpha) to beta * y in
+// its row's stored order (kernel.cc:791, 580-582: separate rounding of every
+// product and sum), so every row summed here is bit-identical to the reference.
+// Slots past a lane's own row length are padding (column 0, value 0) and are not
+// added.  Rows longer than the layout's cap run as the stream plan's long-row chunks
+// (launch_spmv_long_rows).
+#include "sm_internal.h"
+#include "sell.h"
+
+namespace smamd {
+namespace {
+
+constexpr int kSellThreads = 256;
+
+template <int U>
+__global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
+    int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+    const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
+    const int32_t *__restrict__ col, const float *__restrict__ val, const float *__restrict__ x,
+    float *__restrict__ y, float alpha, float beta) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * (kSellThreads / 64) + (threadIdx.x >> 6);
+    if (s >= n_slices) return;   // wave-uniform
+    const int64_t base = off[s];
+    const int32_t L = len[s];
+    const int32_t r = row[s * kSellLanes + lane];
+    const int32_t n = row_len[s * kSellLanes + lane];
+    float acc = r >= 0 ? y[r] : 0.0f;
+    if (beta != 1.0f) acc = __fmul_rn(acc, beta);
+    const int32_t *c = col + base + lane;
+    const float *v = val + base + lane;
+    for (int32_t j = 0; j < L; j += U) {
+        int32_t cc[U];
+        float vv[U], xg[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            cc[u] = __builtin_nontemporal_load(c + (int64_t)(j + u) * kSellLanes);
+            vv[u] = __builtin_nontemporal_load(v + (int64_t)(j + u) * kSellLanes);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xg[u] = x[cc[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float t = __fmul_rn(xg[u], __fmul_rn(vv[u], alpha));
+            if (j + u < n) acc = __fadd_rn(acc, t);
+        }
+    }
+    if (r >= 0) y[r] = acc;
+}
+
+}  // namespace
+
+hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float alpha, float beta,
+                            hipStream_t s) {
+    if (sd.n_slices <= 0) return hipSuccess;
+    if (!sd.d_off || !sd.d_len || !sd.d_row || !sd.d_row_len || !sd.d_col || !sd.d_val)
+        return hipErrorInvalidValue;
+    const int64_t grid = (sd.n_slices + kSellThreads / 64 - 1) / (kSellThreads / 64);
+    if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
+    static_assert(kSellUnroll % 8 == 0, "slice lengths are multiples of the unroll");
+    hipLaunchKernelGGL((spmv_sell_kernel<8>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
+                       sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col, sd.d_val,
+                       x, y, alpha, beta);
+    return hipGetLastError();
+}
+
+}  // namespace smamd

@@ -55,8 +55,20 @@ struct XbandDev {
     int32_t table_size = 0;
 };
 
+// Device copy of the sorted sliced-ELL layout (sell.h).
+struct SellDev {
+    int64_t n_slices = 0;             // 0 when not built
+    int64_t *d_off = nullptr;         // n_slices
+    int32_t *d_len = nullptr;         // n_slices
+    int32_t *d_row = nullptr;         // n_slices * 64 (-1: no row)
+    int32_t *d_row_len = nullptr;     // n_slices * 64
+    int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
+    float *d_val = nullptr;
+};
+
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
+    SellDev sell;                     // n_slices == 0 when not built
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -85,6 +97,13 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               float beta, float *partials, hipStream_t s);
 hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
+// Sorted sliced-ELL (kernels_sell.hip): rows up to the plan's tile size.
+hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float alpha, float beta,
+                            hipStream_t s);
+// Only the stream plan's long rows (chunks + ordered finalize), for the sell path.
+hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t *col,
+                                 const float *val, const float *x, float *y, float alpha,
+                                 float beta, float *partials, hipStream_t s);
 // Balanced-band kind (kernels_band2.hip).
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
