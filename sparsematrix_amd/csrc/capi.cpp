@@ -96,6 +96,10 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.sell.d_row_len);
     (void)hipFree(m->plan.sell.d_col);
     (void)hipFree(m->plan.sell.d_val);
+    (void)hipFree(m->plan.sl_long_rows);
+    (void)hipFree(m->plan.sl_long_ptr);
+    (void)hipFree(m->plan.sl_chunks);
+    (void)hipFree(m->plan.sl_partials);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
     m->d_ws = nullptr;
@@ -380,7 +384,9 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
     SM_TRY_HIP(dev_alloc(&p.d_perm, nc + 4, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_rcol, nnz + kPadElems, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_xperm, nc + 4, m->device_bytes));
-    SM_TRY_HIP(hipMemcpy(p.d_perm, perm.data(), (size_t)nc * 4, hipMemcpyHostToDevice));
+    // The SpMV permutes x by scattering it (coalesced reads, stores that never stall):
+    // the device keeps the original -> new map.
+    SM_TRY_HIP(hipMemcpy(p.d_perm, rank.data(), (size_t)nc * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(p.d_rcol, rcol.data(), (size_t)nnz * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemset(p.d_rcol + nnz, 0, kPadElems * sizeof(int32_t)));
     p.n_relabel = nc;
@@ -407,18 +413,44 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
         SM_TRY_HIP(hipMemcpy(rcol.data(), p.d_rcol, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
         c = rcol.data();
     }
+    // Rows up to max_len terms go to the slices (one lane each, in stored order); the
+    // longer ones run as kLongChunk-term chunks.  SM_SELL_MAX overrides the cap.
+    int32_t max_len = kSellMaxLen;
+    if (const char *e = getenv("SM_SELL_MAX")) max_len = std::max(1, atoi(e));
     SellHost sh;
-    sell_build(rp, c, val, m->n_rows, p.tile_nnz, sh);   // longer rows: the plan's long rows
+    sell_build(rp, c, val, m->n_rows, max_len, sh);
     std::vector<int32_t>().swap(rcol);
     if (sh.n_slices == 0) return SM_OK;
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
+    PlanHost lh;   // long rows: every row > max_len is a "long row" of the planner
+    plan_rows(rp, m->n_rows, max_len, kTileRows, kLongChunk, kSerialRowMax, lh);
+    std::vector<Chunk> chunks(lh.chunks.size());
+    for (size_t i = 0; i < chunks.size(); i++)
+        chunks[i] = Chunk{lh.chunks[i].lr, lh.chunks[i].begin, lh.chunks[i].end, 0};
+    p.sl_n_long = (int32_t)lh.long_rows.size();
+    p.sl_n_chunks = (int32_t)chunks.size();
+    SM_TRY_HIP(dev_alloc(&p.sl_chunks, p.sl_n_chunks, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.sl_partials, p.sl_n_chunks, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.sl_long_rows, p.sl_n_long, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.sl_long_ptr, p.sl_n_long + 1, m->device_bytes));
+    if (p.sl_n_chunks)
+        SM_TRY_HIP(hipMemcpy(p.sl_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice));
+    if (p.sl_n_long) {
+        SM_TRY_HIP(hipMemcpy(p.sl_long_rows, lh.long_rows.data(), lh.long_rows.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(p.sl_long_ptr, lh.long_ptr.data(), lh.long_ptr.size() * 4, hipMemcpyHostToDevice));
+    }
     SellDev &d = p.sell;
+    d.max_len = max_len;
     SM_TRY_HIP(dev_alloc(&d.d_off, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_len, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_row, sh.n_slices * kSellLanes, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_row_len, sh.n_slices * kSellLanes, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_col, sh.padded, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_val, sh.padded, m->device_bytes));
+    // + a zeroed tail of 32 slots per lane: unrolls past kSellUnroll read up to it.
+    const int64_t tail = 32 * kSellLanes;
+    SM_TRY_HIP(dev_alloc(&d.d_col, sh.padded + tail, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_val, sh.padded + tail, m->device_bytes));
+    SM_TRY_HIP(hipMemset(d.d_col + sh.padded, 0, (size_t)tail * 4));
+    SM_TRY_HIP(hipMemset(d.d_val + sh.padded, 0, (size_t)tail * 4));
     SM_TRY_HIP(hipMemcpy(d.d_off, sh.off.data(), sh.off.size() * 8, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_len, sh.len.data(), sh.len.size() * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_row, sh.row.data(), sh.row.size() * 4, hipMemcpyHostToDevice));

@@ -485,15 +485,27 @@ __global__ __launch_bounds__(256) void scatter_dense_kernel(int32_t n, const int
 
 // xp[i] = x[perm[i]]: 4 outputs per thread (one 16-byte load of perm, four
 // gathers in flight, one 16-byte store); the tail (n % 4) one by one.
-__global__ __launch_bounds__(256) void x_relabel_kernel(int64_t n, const int32_t *__restrict__ perm,
+// xp[rank[c]] = x[c]: coalesced reads of x and rank, scattered stores (nothing waits
+// on a store; a gather xp[i] = x[perm[i]] exposed one read latency per element).
+template <bool VEC>
+__global__ __launch_bounds__(256) void x_relabel_kernel(int64_t n, const int32_t *__restrict__ rank,
                                                         const float *__restrict__ x,
                                                         float *__restrict__ xp) {
-    const int64_t i = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
-    if (i + 4 <= n) {
-        const int4 p = *reinterpret_cast<const int4 *>(perm + i);
-        *reinterpret_cast<float4 *>(xp + i) = make_float4(x[p.x], x[p.y], x[p.z], x[p.w]);
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if constexpr (VEC) {
+        const int64_t i = 4 * t;
+        if (i + 4 <= n) {
+            const int4 r = *reinterpret_cast<const int4 *>(rank + i);
+            const float4 v = *reinterpret_cast<const float4 *>(x + i);
+            xp[r.x] = v.x;
+            xp[r.y] = v.y;
+            xp[r.z] = v.z;
+            xp[r.w] = v.w;
+        } else {
+            for (int64_t k = i; k < n; ++k) xp[rank[k]] = x[k];
+        }
     } else {
-        for (int64_t k = i; k < n; ++k) xp[k] = x[perm[k]];
+        if (t < n) xp[rank[t]] = x[t];
     }
 }
 
@@ -547,23 +559,16 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
 hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t *col,
                                  const float *val, const float *x, float *y, float alpha,
                                  float beta, float *partials, hipStream_t s) {
-    if (p.n_chunks == 0) return hipSuccess;
-    // Blocks [0, n_chunks) of the stream kernel are the long-row chunks; no tile runs.
-#define SM_LONG(TT)                                                                           \
-    case TT:                                                                                  \
-        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)p.n_chunks), \
-                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp,  \
-                           col, val, x, y, alpha, beta, partials);                            \
-        break;
-    switch (p.tile_nnz) {
-        SM_LONG(1024) SM_LONG(2048) SM_LONG(4096) SM_LONG(8192)
-        default: return hipErrorInvalidValue;
-    }
-#undef SM_LONG
+    (void)partials;
+    if (p.sl_n_chunks == 0) return hipSuccess;
+    // The stream kernel's chunk blocks over the sell path's long rows; no tile runs.
+    hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, kLongChunk>), dim3((unsigned)p.sl_n_chunks),
+                       dim3(kStreamThreads), 0, s, nullptr, p.sl_chunks, p.sl_n_chunks, rp, col,
+                       val, x, y, alpha, beta, p.sl_partials);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.n_long)), dim3(256), 0, s,
-                       p.n_long, p.d_long_rows, p.d_long_ptr, partials, y, beta);
+    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.sl_n_long)), dim3(256), 0, s,
+                       p.sl_n_long, p.sl_long_rows, p.sl_long_ptr, p.sl_partials, y, beta);
     return hipGetLastError();
 }
 
@@ -654,11 +659,15 @@ hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const in
     return hipGetLastError();
 }
 
-hipError_t launch_x_relabel(int64_t n, const int32_t *perm, const float *x, float *xp,
+hipError_t launch_x_relabel(int64_t n, const int32_t *rank, const float *x, float *xp,
                             hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(x_relabel_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, s, n, perm,
-                       x, xp);
+    if (((uintptr_t)x & 15) == 0)
+        hipLaunchKernelGGL(x_relabel_kernel<true>, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, s,
+                           n, rank, x, xp);
+    else
+        hipLaunchKernelGGL(x_relabel_kernel<false>, dim3(blocks_for(n)), dim3(256), 0, s, n, rank,
+                           x, xp);
     return hipGetLastError();
 }
 

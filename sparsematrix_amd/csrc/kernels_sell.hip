@@ -12,12 +12,16 @@
 #include "sm_internal.h"
 #include "sell.h"
 
+#include <cstdlib>
+
 namespace smamd {
 namespace {
 
 constexpr int kSellThreads = 256;
 
-template <int U>
+// ABL (development only, SM_SELL_ABLATE; results wrong): 1 replaces the x gathers by
+// one broadcast address.
+template <int U, int ABL = 0>
 __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
@@ -43,7 +47,7 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
             vv[u] = __builtin_nontemporal_load(v + (int64_t)(j + u) * kSellLanes);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) xg[u] = x[cc[u]];
+        for (int u = 0; u < U; ++u) xg[u] = x[(ABL & 1) ? (cc[u] & 0) : cc[u]];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float t = __fmul_rn(xg[u], __fmul_rn(vv[u], alpha));
@@ -63,9 +67,25 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
     const int64_t grid = (sd.n_slices + kSellThreads / 64 - 1) / (kSellThreads / 64);
     if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
     static_assert(kSellUnroll % 8 == 0, "slice lengths are multiples of the unroll");
-    hipLaunchKernelGGL((spmv_sell_kernel<8>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
-                       sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col, sd.d_val,
-                       x, y, alpha, beta);
+    // Unrolls past kSellUnroll read slots past a slice's padded length: those lanes'
+    // row lengths stop the adds, and the reads stay inside the arrays' zero tail.
+    static const int abl = [] {
+        const char *e = getenv("SM_SELL_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+#define SM_SELL_K(U, A)                                                                        \
+    hipLaunchKernelGGL((spmv_sell_kernel<U, A>), dim3((unsigned)grid), dim3(kSellThreads), 0, s, \
+                       sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col,       \
+                       sd.d_val, x, y, alpha, beta)
+    static const int unroll = [] {
+        const char *e = getenv("SM_SELL_UNROLL");
+        return e ? atoi(e) : 8;
+    }();
+    if (abl == 1) SM_SELL_K(8, 1);
+    else if (unroll == 16) SM_SELL_K(16, 0);
+    else if (unroll == 32) SM_SELL_K(32, 0);
+    else SM_SELL_K(8, 0);
+#undef SM_SELL_K
     return hipGetLastError();
 }
 

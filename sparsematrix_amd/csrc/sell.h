@@ -9,6 +9,7 @@ namespace smamd {
 
 constexpr int kSellLanes = 64;    // rows per slice: one wavefront
 constexpr int kSellUnroll = 8;    // slice lengths are padded to a multiple of this
+constexpr int kSellMaxLen = 2048;  // longer rows run as long-row chunks (tree sums)
 
 // Rows of at most `max_len` terms, sorted by length (longest first, ties in row
 // order), cut into slices of 64; slice s holds its rows' terms column-interleaved:

@@ -64,11 +64,17 @@ struct SellDev {
     int32_t *d_row_len = nullptr;     // n_slices * 64
     int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
     float *d_val = nullptr;
+    int32_t max_len = 0;              // rows up to this length are in the slices
 };
 
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
+    // The sell path's long rows (> sell.max_len): chunks as below, own arrays.
+    int32_t sl_n_long = 0, sl_n_chunks = 0;
+    int32_t *sl_long_rows = nullptr, *sl_long_ptr = nullptr;
+    Chunk *sl_chunks = nullptr;
+    float *sl_partials = nullptr;
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -84,7 +90,7 @@ struct Plan {
     // columns renumbered by descending number of terms, so the hot part of x is
     // a dense prefix that stays in L2.  Terms keep their stored order (bit-identical).
     int64_t n_relabel = 0;            // n_cols when built, else 0
-    int32_t *d_perm = nullptr;        // new column -> original column
+    int32_t *d_perm = nullptr;        // original column -> new column (x is scattered)
     int32_t *d_rcol = nullptr;        // relabeled col_idx (nnz + kPadElems, zero tail)
     float *d_xperm = nullptr;         // x in the new numbering (one SpMV in flight)
 };
@@ -107,8 +113,8 @@ hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t
 // Balanced-band kind (kernels_band2.hip).
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
-// xp[i] = x[perm[i]], i < n.
-hipError_t launch_x_relabel(int64_t n, const int32_t *perm, const float *x, float *xp,
+// xp[rank[c]] = x[c], c < n (rank: original column -> new column).
+hipError_t launch_x_relabel(int64_t n, const int32_t *rank, const float *x, float *xp,
                             hipStream_t s);
 hipError_t launch_spmv_vector(int32_t n, double avg_row, const int32_t *rp, const int32_t *col,
                               const float *val, const float *x, float *y, float alpha, float beta,
