@@ -1,0 +1,75 @@
+// Host-only check of the sorted sliced-ELL builder (sparsematrix_amd/csrc/sell.cpp),
+// built with AddressSanitizer by tests/test_xband_builder.py.  For random and skewed
+// shapes: every row of at most max_len terms sits in exactly one lane with its terms
+// in stored order, longer rows in none, slices are sorted by length (longest first)
+// and padded to multiples of kSellUnroll with column 0 / value 0, lanes past the
+// rows hold -1.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "sell.h"
+
+using namespace smamd;
+
+static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
+                 const std::vector<float> &val, int64_t n_rows, int32_t max_len) {
+    SellHost h;
+    sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h);
+    std::vector<int> seen((size_t)n_rows, 0);
+    int64_t slots = 0;
+    int32_t prev_len = INT32_MAX;
+    for (int64_t s = 0; s < h.n_slices; s++) {
+        const int32_t L = h.len[(size_t)s];
+        if (h.off[(size_t)s] != slots || L % kSellUnroll) { printf("FAIL slice offsets\n"); return 1; }
+        slots += (int64_t)L * kSellLanes;
+        for (int l = 0; l < kSellLanes; l++) {
+            const int32_t r = h.row[(size_t)(s * kSellLanes + l)];
+            const int32_t n = h.row_len[(size_t)(s * kSellLanes + l)];
+            if (r < 0) {
+                if (n != 0) { printf("FAIL empty lane\n"); return 1; }
+                for (int32_t j = 0; j < L; j++)
+                    if (h.col[(size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l)] != 0) { printf("FAIL pad\n"); return 1; }
+                continue;
+            }
+            if (r >= n_rows || n != rp[r + 1] - rp[r] || n > max_len || n > L) { printf("FAIL row\n"); return 1; }
+            if (n > prev_len) { printf("FAIL order\n"); return 1; }
+            prev_len = n;
+            seen[(size_t)r]++;
+            for (int32_t j = 0; j < L; j++) {
+                const size_t k = (size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l);
+                const int32_t c = j < n ? col[rp[r] + j] : 0;
+                const float v = j < n ? val[rp[r] + j] : 0.0f;
+                if (h.col[k] != c || h.val[k] != v) { printf("FAIL term\n"); return 1; }
+            }
+        }
+    }
+    if (slots != h.padded || (int64_t)h.col.size() != slots) { printf("FAIL sizes\n"); return 1; }
+    for (int64_t r = 0; r < n_rows; r++) {
+        const bool want = rp[r + 1] - rp[r] <= max_len;
+        if (seen[(size_t)r] != (want ? 1 : 0)) { printf("FAIL coverage row %lld\n", (long long)r); return 1; }
+    }
+    return 0;
+}
+
+int main() {
+    int bad = 0;
+    std::mt19937 rng(5);
+    for (int64_t n_rows : {1, 63, 64, 65, 1000, 70001}) {
+        for (int skew = 0; skew < 2; skew++) {
+            std::vector<int32_t> rp((size_t)n_rows + 1, 0), col;
+            std::vector<float> val;
+            for (int64_t r = 0; r < n_rows; r++) {
+                int32_t n = skew ? (int32_t)(std::pow(1.0 - (rng() % 10000) / 10000.0, -1.5) - 1) : (int32_t)(rng() % 20);
+                n = std::min<int32_t>(n, 5000);
+                for (int32_t j = 0; j < n; j++) { col.push_back((int32_t)(rng() % 100000)); val.push_back((float)(rng() % 97) - 48.0f); }
+                rp[(size_t)r + 1] = (int32_t)col.size();
+            }
+            for (int32_t mx : {1, 16, 2048}) bad += check(rp, col, val, n_rows, mx);
+        }
+    }
+    printf(bad ? "sell_asan: FAILED\n" : "sell_asan: ok\n");
+    return bad ? 1 : 0;
+}

@@ -39,3 +39,19 @@ def test_band2_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "band2_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_sell_builder_under_asan(tmp_path):
+    """Sorted sliced-ELL builder (sell.cpp): every short row in exactly one lane with its
+    terms in stored order, slices sorted and padded, long rows left out."""
+    exe = tmp_path / "sell_asan"
+    src = [os.path.join(ROOT, "tests", "native", "sell_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "sell.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sell_asan: ok" in r.stdout
