@@ -767,3 +767,43 @@ def test_addmatmat_workspace_back_to_back(sm):
     torch.cuda.synchronize()
     for (A, _, want), (_, c_d) in zip(cases[:2], dev):
         assert bits_equal(to_host(c_d).reshape(A.shape[0], n), want), A.shape[0]
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_spmv_cband_and_sell(sm, name):
+    """The round-2 SpMV layouts against the reference's own AddMatMat outputs (m = 1
+    runs): cband forced with one slab (every row in the reference's order) and the
+    sorted sliced-ELL layout are both bit-identical to the compiled reference."""
+    c = load_case(name)
+    if not c.runs:
+        pytest.skip("no AddMatMat runs")
+    k, n = c.s_rows, c.s_cols
+
+    def build(env):
+        def go(items):
+            if not items:
+                return _from_case(sm, c)
+            (key, v), rest = items[0], items[1:]
+            return _with_env(key, v, lambda: go(rest))
+        return go(list(env.items()))
+
+    layouts = {
+        "cband": build({"SM_XBAND": "1", "SM_XBAND_KIND": "cband", "SM_BAND2_SLABS": "1"}),
+        "sell": build({"SM_XBAND": "0", "SM_SELL": "1"}),
+    }
+    rp, _, _ = layouts["sell"].csr()
+    for lay, M in layouts.items():
+        info = M.info()
+        if rp[-1] == 0:
+            continue   # no terms: no layout is built, AUTO runs the beta pass only
+        if lay == "cband":
+            assert info["has_xband"] == 5 and info["xband_slabs"] == 1, info
+        else:
+            assert info["sell_slices"] > 0, info
+        for r in c.runs:
+            A = r.a.reshape(r.m, r.lda)[:, :k]
+            Cin = r.c.reshape(r.m, r.ldc)[:, :n]
+            want = r.out.reshape(r.m, r.ldc)[:, :n]
+            y = to_dev(Cin[0].copy())
+            M.spmv(to_dev(A[0].copy()), y, r.alpha, r.beta, algo="auto")
+            assert bits_equal(to_host(y), want[0]), (lay, r.alpha, r.beta)
