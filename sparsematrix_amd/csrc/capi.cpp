@@ -441,6 +441,7 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     }
     SellDev &d = p.sell;
     d.max_len = max_len;
+    d.n_cols = m->n_cols;
     SM_TRY_HIP(dev_alloc(&d.d_off, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_len, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_row, sh.n_slices * kSellLanes, m->device_bytes));

@@ -65,6 +65,7 @@ struct SellDev {
     int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
     float *d_val = nullptr;
     int32_t max_len = 0;              // rows up to this length are in the slices
+    int64_t n_cols = 0;               // x length (the hot-prefix variant)
 };
 
 struct Plan {

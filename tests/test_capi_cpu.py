@@ -95,3 +95,30 @@ def test_python_mirror_surface():
                  "SelfTest", "__eq__", "spmv", "spmm", "from_csr"):
         assert hasattr(smd.SparseMatrix, name)
     assert smd.SblasNoTrans == 0 and smd.SblasTrans == 1
+
+
+def test_header_and_python_mirror_agree():
+    """The sm_algo values and the sm_info layout the Python mirror uses match the C
+    header (a struct mismatch would let sm_get_info write past the ctypes buffer)."""
+    import ctypes
+    import re
+    import subprocess
+    import tempfile
+
+    from sparsematrix_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "sparsematrix.h")).read()
+    for name, val in _lib.ALGOS.items():
+        m = re.search(r"SM_ALGO_%s\s*=\s*(\d+)" % name.upper(), hdr)
+        assert m and int(m.group(1)) == val, name
+    src = ('#include <stddef.h>\n#include <stdio.h>\n#include "sparsematrix.h"\n'
+           'int main(void){printf("%zu %zu\\n", sizeof(sm_info), offsetof(sm_info, sell_slices));'
+           'return 0;}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        size, off = map(int, subprocess.run([exe], capture_output=True, text=True,
+                                            check=True).stdout.split())
+    assert ctypes.sizeof(_lib.SmInfo) == size
+    assert _lib.SmInfo.sell_slices.offset == off
