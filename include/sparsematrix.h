@@ -72,9 +72,9 @@ typedef enum sm_algo {
     SM_ALGO_XBAND = 4,    /* x staged through LDS in column bands (the layout built at
                              creation, see sm_info.has_xband); falls back to SELL, then
                              STREAM, when the matrix holds no band layout             */
-    SM_ALGO_SELL = 5      /* sorted sliced-ELL, one lane per row (every row up to the
-                             stream tile size bit-identical; longer rows as the stream
-                             plan's chunks); STREAM when the layout is not built       */
+    SM_ALGO_SELL = 5      /* sorted sliced-ELL, one lane per row (every row up to 2048
+                             terms bit-identical; longer rows in 2048-term segments whose
+                             sums are added in order); STREAM when not built           */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the

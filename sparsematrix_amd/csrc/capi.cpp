@@ -96,10 +96,9 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.sell.d_row_len);
     (void)hipFree(m->plan.sell.d_col);
     (void)hipFree(m->plan.sell.d_val);
-    (void)hipFree(m->plan.sl_long_rows);
-    (void)hipFree(m->plan.sl_long_ptr);
-    (void)hipFree(m->plan.sl_chunks);
-    (void)hipFree(m->plan.sl_partials);
+    (void)hipFree(m->plan.sell.d_long_rows);
+    (void)hipFree(m->plan.sell.d_long_ptr);
+    (void)hipFree(m->plan.sell.d_partials);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
     m->d_ws = nullptr;
@@ -414,7 +413,7 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
         c = rcol.data();
     }
     // Rows up to max_len terms go to the slices (one lane each, in stored order); the
-    // longer ones run as kLongChunk-term chunks.  SM_SELL_MAX overrides the cap.
+    // longer ones as max_len-term segments.  SM_SELL_MAX overrides the cap.
     int32_t max_len = kSellMaxLen;
     if (const char *e = getenv("SM_SELL_MAX")) max_len = std::max(1, atoi(e));
     SellHost sh;
@@ -422,26 +421,18 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     std::vector<int32_t>().swap(rcol);
     if (sh.n_slices == 0) return SM_OK;
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
-    PlanHost lh;   // long rows: every row > max_len is a "long row" of the planner
-    plan_rows(rp, m->n_rows, max_len, kTileRows, kLongChunk, kSerialRowMax, lh);
-    std::vector<Chunk> chunks(lh.chunks.size());
-    for (size_t i = 0; i < chunks.size(); i++)
-        chunks[i] = Chunk{lh.chunks[i].lr, lh.chunks[i].begin, lh.chunks[i].end, 0};
-    p.sl_n_long = (int32_t)lh.long_rows.size();
-    p.sl_n_chunks = (int32_t)chunks.size();
-    SM_TRY_HIP(dev_alloc(&p.sl_chunks, p.sl_n_chunks, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&p.sl_partials, p.sl_n_chunks, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&p.sl_long_rows, p.sl_n_long, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&p.sl_long_ptr, p.sl_n_long + 1, m->device_bytes));
-    if (p.sl_n_chunks)
-        SM_TRY_HIP(hipMemcpy(p.sl_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice));
-    if (p.sl_n_long) {
-        SM_TRY_HIP(hipMemcpy(p.sl_long_rows, lh.long_rows.data(), lh.long_rows.size() * 4, hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(p.sl_long_ptr, lh.long_ptr.data(), lh.long_ptr.size() * 4, hipMemcpyHostToDevice));
-    }
     SellDev &d = p.sell;
     d.max_len = max_len;
     d.n_cols = m->n_cols;
+    d.n_long = (int32_t)sh.long_rows.size();
+    const int32_t n_parts = sh.long_ptr.back();
+    SM_TRY_HIP(dev_alloc(&d.d_long_rows, d.n_long, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_long_ptr, d.n_long + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_partials, n_parts, m->device_bytes));
+    if (d.n_long) {
+        SM_TRY_HIP(hipMemcpy(d.d_long_rows, sh.long_rows.data(), sh.long_rows.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_long_ptr, sh.long_ptr.data(), sh.long_ptr.size() * 4, hipMemcpyHostToDevice));
+    }
     SM_TRY_HIP(dev_alloc(&d.d_off, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_len, sh.n_slices, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_row, sh.n_slices * kSellLanes, m->device_bytes));
@@ -996,16 +987,11 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     case SM_ALGO_SELL:
         if (m->plan.sell.n_slices > 0) {
             const float *xs = x;
-            const int32_t *lc = m->d_col;
-            if (m->plan.n_relabel > 0) {
+            if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns
                 e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
                 xs = m->plan.d_xperm;
-                lc = m->plan.d_rcol;
             }
             if (e == hipSuccess) e = launch_spmv_sell(m->plan.sell, xs, y, alpha, beta, s);
-            if (e == hipSuccess)
-                e = launch_spmv_long_rows(m->plan, m->d_row_ptr, lc, m->d_val, xs, y, alpha, beta,
-                                          m->plan.d_partials, s);
             break;
         }
         [[fallthrough]];   // no sell layout -> stream kernel

@@ -556,19 +556,11 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
     return hipGetLastError();
 }
 
-hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t *col,
-                                 const float *val, const float *x, float *y, float alpha,
-                                 float beta, float *partials, hipStream_t s) {
-    (void)partials;
-    if (p.sl_n_chunks == 0) return hipSuccess;
-    // The stream kernel's chunk blocks over the sell path's long rows; no tile runs.
-    hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, kLongChunk>), dim3((unsigned)p.sl_n_chunks),
-                       dim3(kStreamThreads), 0, s, nullptr, p.sl_chunks, p.sl_n_chunks, rp, col,
-                       val, x, y, alpha, beta, p.sl_partials);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.sl_n_long)), dim3(256), 0, s,
-                       p.sl_n_long, p.sl_long_rows, p.sl_long_ptr, p.sl_partials, y, beta);
+hipError_t launch_long_finalize(int32_t n_long, const int32_t *long_rows, const int32_t *long_ptr,
+                                const float *partials, float *y, float beta, hipStream_t s) {
+    if (n_long <= 0) return hipSuccess;
+    hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(n_long)), dim3(256), 0, s, n_long,
+                       long_rows, long_ptr, partials, y, beta);
     return hipGetLastError();
 }
 

@@ -5,10 +5,12 @@
 // of its slice; slot j of the 64 lanes is one coalesced 256-byte load of columns and
 // one of values, then 64 x gathers.  Each lane adds x * (v * alpha) to beta * y in
 // its row's stored order (kernel.cc:791, 580-582: separate rounding of every
-// product and sum), so every row summed here is bit-identical to the reference.
-// Slots past a lane's own row length are padding (column 0, value 0) and are not
-// added.  Rows longer than the layout's cap run as the stream plan's long-row chunks
-// (launch_spmv_long_rows).
+// product and sum), so every row of up to kSellMaxLen terms is bit-identical to the
+// reference.  Slots past a lane's own length are padding (column 0, value 0) and are
+// not added.  Longer rows are cut in kSellMaxLen-term segments that sit in the slices
+// like rows; each segment's sum (from -0.0) goes to a partial, and the finalize adds
+// beta * y and the partials in segment order (deterministic, within the Sum|terms|
+// bound).
 #include "sm_internal.h"
 #include "sell.h"
 
@@ -27,7 +29,7 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
     const int32_t *__restrict__ col, const float *__restrict__ val, const float *__restrict__ x,
-    float *__restrict__ y, float alpha, float beta) {
+    float *__restrict__ y, float *__restrict__ partials, float alpha, float beta) {
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * (kSellThreads / 64) + (threadIdx.x >> 6);
     if (s >= n_slices) return;   // wave-uniform
@@ -35,8 +37,10 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
     const int32_t L = len[s];
     const int32_t r = row[s * kSellLanes + lane];
     const int32_t n = row_len[s * kSellLanes + lane];
-    float acc = r >= 0 ? y[r] : 0.0f;
-    if (beta != 1.0f) acc = __fmul_rn(acc, beta);
+    // A row starts from beta * y; a long row's segment from -0.0 (the identity of fp32
+    // addition), its sum going to the segment's partial.
+    float acc = r >= 0 ? y[r] : -0.0f;
+    if (r >= 0 && beta != 1.0f) acc = __fmul_rn(acc, beta);
     const int32_t *c = col + base + lane;
     const float *v = val + base + lane;
     for (int32_t j = 0; j < L; j += U) {
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(1024) void spmv_sell_hot_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
     const int32_t *__restrict__ col, const float *__restrict__ val, const float *__restrict__ x,
-    int64_t n_cols, float *__restrict__ y, float alpha, float beta) {
+    int64_t n_cols, float *__restrict__ y, float *__restrict__ partials, float alpha, float beta) {
     __shared__ __attribute__((aligned(16))) float xh[H];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -84,8 +88,8 @@ __global__ __launch_bounds__(1024) void spmv_sell_hot_kernel(
         const int32_t L = len[s];
         const int32_t r = row[s * kSellLanes + lane];
         const int32_t n = row_len[s * kSellLanes + lane];
-        float acc = r >= 0 ? y[r] : 0.0f;
-        if (beta != 1.0f) acc = __fmul_rn(acc, beta);
+        float acc = r >= 0 ? y[r] : -0.0f;
+        if (r >= 0 && beta != 1.0f) acc = __fmul_rn(acc, beta);
         const int32_t *c = col + base + lane;
         const float *v = val + base + lane;
         for (int32_t j = 0; j < L; j += U) {
@@ -112,6 +116,7 @@ __global__ __launch_bounds__(1024) void spmv_sell_hot_kernel(
             }
         }
         if (r >= 0) y[r] = acc;
+        else if (r < -1) partials[-2 - r] = acc;
     }
 }
 
@@ -134,7 +139,7 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
 #define SM_SELL_K(U, A)                                                                        \
     hipLaunchKernelGGL((spmv_sell_kernel<U, A>), dim3((unsigned)grid), dim3(kSellThreads), 0, s, \
                        sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col,       \
-                       sd.d_val, x, y, alpha, beta)
+                       sd.d_val, x, y, sd.d_partials, alpha, beta)
     static const int unroll = [] {
         const char *e = getenv("SM_SELL_UNROLL");
         return e ? atoi(e) : 8;
@@ -150,7 +155,11 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         const int64_t wgs = std::min<int64_t>(2 * (int64_t)n_cu, (sd.n_slices + 15) / 16);
         hipLaunchKernelGGL((spmv_sell_hot_kernel<8, 16384>), dim3((unsigned)wgs), dim3(1024), 0, s,
                            sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col,
-                           sd.d_val, x, sd.n_cols, y, alpha, beta);
+                           sd.d_val, x, sd.n_cols, y, sd.d_partials, alpha, beta);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? launch_long_finalize(sd.n_long, sd.d_long_rows, sd.d_long_ptr,
+                                                      sd.d_partials, y, beta, s)
+                               : e;
         return hipGetLastError();
     }
     if (abl == 1) SM_SELL_K(8, 1);
@@ -158,7 +167,10 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
     else if (unroll == 32) SM_SELL_K(32, 0);
     else SM_SELL_K(8, 0);
 #undef SM_SELL_K
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // Long rows: beta * y + their segment partials, in segment order.
+    return launch_long_finalize(sd.n_long, sd.d_long_rows, sd.d_long_ptr, sd.d_partials, y, beta, s);
 }
 
 }  // namespace smamd

@@ -13,28 +13,40 @@ namespace smamd {
 void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
                 int32_t max_len, SellHost &out) {
     out = SellHost();
-    // Counting sort by descending length (stable: ties keep row order).
+    // Units: a row of <= max_len terms, or one segment of a longer row.
+    struct Unit {
+        int32_t row, start, n, part;   // part >= 0: segment partial index
+    };
+    std::vector<Unit> units;
+    units.reserve((size_t)n_rows);
+    out.long_ptr.push_back(0);
+    int32_t parts = 0;
+    for (int64_t r = 0; r < n_rows; r++) {
+        const int32_t a = rp[r], l = rp[r + 1] - a;
+        if (l <= max_len) {
+            units.push_back(Unit{(int32_t)r, a, l, -1});
+            continue;
+        }
+        for (int32_t b = 0; b < l; b += max_len)
+            units.push_back(Unit{(int32_t)r, a + b, std::min(max_len, l - b), parts++});
+        out.long_rows.push_back((int32_t)r);
+        out.long_ptr.push_back(parts);
+    }
+    // Counting sort by descending length (stable: ties keep row / segment order).
     std::vector<int64_t> cnt((size_t)max_len + 2, 0);
-    int64_t n_short = 0;
-    for (int64_t r = 0; r < n_rows; r++) {
-        const int32_t l = rp[r + 1] - rp[r];
-        if (l <= max_len) { cnt[(size_t)(max_len - l) + 1]++; n_short++; }
-    }
+    for (const Unit &u : units) cnt[(size_t)(max_len - u.n) + 1]++;
     for (size_t i = 1; i < cnt.size(); i++) cnt[i] += cnt[i - 1];
-    std::vector<int32_t> order((size_t)n_short);
-    for (int64_t r = 0; r < n_rows; r++) {
-        const int32_t l = rp[r + 1] - rp[r];
-        if (l <= max_len) order[(size_t)cnt[(size_t)(max_len - l)]++] = (int32_t)r;
-    }
-    out.n_slices = (n_short + kSellLanes - 1) / kSellLanes;
+    std::vector<int32_t> order(units.size());
+    for (size_t i = 0; i < units.size(); i++) order[(size_t)cnt[(size_t)(max_len - units[i].n)]++] = (int32_t)i;
+    const int64_t n_units = (int64_t)units.size();
+    out.n_slices = (n_units + kSellLanes - 1) / kSellLanes;
     out.off.resize((size_t)out.n_slices);
     out.len.resize((size_t)out.n_slices);
     out.row.assign((size_t)out.n_slices * kSellLanes, -1);
     out.row_len.assign((size_t)out.n_slices * kSellLanes, 0);
     int64_t slots = 0;
     for (int64_t s = 0; s < out.n_slices; s++) {
-        const int32_t r0 = order[(size_t)(s * kSellLanes)];   // the slice's longest row
-        const int32_t L = rp[r0 + 1] - rp[r0];
+        const int32_t L = units[(size_t)order[(size_t)(s * kSellLanes)]].n;   // the slice's longest
         out.off[(size_t)s] = slots;
         out.len[(size_t)s] = (L + kSellUnroll - 1) / kSellUnroll * kSellUnroll;
         slots += (int64_t)out.len[(size_t)s] * kSellLanes;
@@ -42,17 +54,16 @@ void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t
     out.padded = slots;
     out.col.assign((size_t)slots, 0);
     out.val.assign((size_t)slots, 0.0f);
-    for (int64_t i = 0; i < n_short; i++) {
+    for (int64_t i = 0; i < n_units; i++) {
         const int64_t s = i / kSellLanes, l = i % kSellLanes;
-        const int32_t r = order[(size_t)i];
-        const int32_t a = rp[r], n = rp[r + 1] - a;
-        out.row[(size_t)i] = r;
-        out.row_len[(size_t)i] = n;
+        const Unit &u = units[(size_t)order[(size_t)i]];
+        out.row[(size_t)i] = u.part >= 0 ? -2 - u.part : u.row;
+        out.row_len[(size_t)i] = u.n;
         int32_t *c = out.col.data() + out.off[(size_t)s] + l;
         float *v = out.val.data() + out.off[(size_t)s] + l;
-        for (int32_t j = 0; j < n; j++) {
-            c[(size_t)j * kSellLanes] = col[a + j];
-            v[(size_t)j * kSellLanes] = val[a + j];
+        for (int32_t j = 0; j < u.n; j++) {
+            c[(size_t)j * kSellLanes] = col[u.start + j];
+            v[(size_t)j * kSellLanes] = val[u.start + j];
         }
     }
 }

@@ -9,13 +9,15 @@ namespace smamd {
 
 constexpr int kSellLanes = 64;    // rows per slice: one wavefront
 constexpr int kSellUnroll = 8;    // slice lengths are padded to a multiple of this
-constexpr int kSellMaxLen = 2048;  // longer rows run as long-row chunks (tree sums)
+constexpr int kSellMaxLen = 2048;  // longer rows are cut in segments of this many terms
 
-// Rows of at most `max_len` terms, sorted by length (longest first, ties in row
-// order), cut into slices of 64; slice s holds its rows' terms column-interleaved:
-// term j of lane l at off[s] + 64 * j + l, j < len[s] (padded with column 0, value 0,
-// never added: a lane stops at its own row length).  Rows longer than max_len are
-// left to the stream plan's long-row chunks.
+// Rows of at most `max_len` terms, and segments of max_len terms of the longer rows,
+// sorted by length (longest first, ties in row / segment order), cut into slices of
+// 64; slice s holds its lanes' terms column-interleaved: term j of lane l at
+// off[s] + 64 * j + l, j < len[s] (padded with column 0, value 0, never added: a lane
+// stops at its own length).  A lane's `row` is the row (>= 0), -1 (no row) or
+// -2 - p for segment partial p: segments of one long row have consecutive partials
+// in order (long_ptr), added to beta * y in that order by the finalize kernel.
 struct SellHost {
     int64_t n_slices = 0;
     int64_t padded = 0;                 // stored slots (terms + padding)
@@ -25,6 +27,8 @@ struct SellHost {
     std::vector<int32_t> row_len;       // n_slices * 64: that row's length
     std::vector<int32_t> col;           // padded slots
     std::vector<float> val;
+    std::vector<int32_t> long_rows;     // rows split in segments
+    std::vector<int32_t> long_ptr;      // long_rows.size() + 1: their partials
 };
 
 // col: the matrix's (possibly relabeled) columns.

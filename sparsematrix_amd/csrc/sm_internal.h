@@ -64,18 +64,18 @@ struct SellDev {
     int32_t *d_row_len = nullptr;     // n_slices * 64
     int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
     float *d_val = nullptr;
-    int32_t max_len = 0;              // rows up to this length are in the slices
+    int32_t max_len = 0;              // rows up to this length are whole lanes
     int64_t n_cols = 0;               // x length (the hot-prefix variant)
+    // Rows longer than max_len: cut in segments (lanes with row = -2 - partial).
+    int32_t n_long = 0;
+    int32_t *d_long_rows = nullptr;   // n_long
+    int32_t *d_long_ptr = nullptr;    // n_long + 1 offsets into d_partials
+    float *d_partials = nullptr;      // one per segment (one SpMV in flight per matrix)
 };
 
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
-    // The sell path's long rows (> sell.max_len): chunks as below, own arrays.
-    int32_t sl_n_long = 0, sl_n_chunks = 0;
-    int32_t *sl_long_rows = nullptr, *sl_long_ptr = nullptr;
-    Chunk *sl_chunks = nullptr;
-    float *sl_partials = nullptr;
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -107,10 +107,9 @@ hipError_t launch_spmv_xband(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
 // Sorted sliced-ELL (kernels_sell.hip): rows up to the plan's tile size.
 hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float alpha, float beta,
                             hipStream_t s);
-// Only the stream plan's long rows (chunks + ordered finalize), for the sell path.
-hipError_t launch_spmv_long_rows(const Plan &p, const int32_t *rp, const int32_t *col,
-                                 const float *val, const float *x, float *y, float alpha,
-                                 float beta, float *partials, hipStream_t s);
+// y[long_rows[i]] = beta * y + partials[long_ptr[i] .. long_ptr[i+1]) in order.
+hipError_t launch_long_finalize(int32_t n_long, const int32_t *long_rows, const int32_t *long_ptr,
+                                const float *partials, float *y, float beta, hipStream_t s);
 // Balanced-band kind (kernels_band2.hip).
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);

@@ -1,9 +1,10 @@
 // Host-only check of the sorted sliced-ELL builder (sparsematrix_amd/csrc/sell.cpp),
 // built with AddressSanitizer by tests/test_xband_builder.py.  For random and skewed
 // shapes: every row of at most max_len terms sits in exactly one lane with its terms
-// in stored order, longer rows in none, slices are sorted by length (longest first)
-// and padded to multiples of kSellUnroll with column 0 / value 0, lanes past the
-// rows hold -1.
+// in stored order, every longer row in consecutive max_len-term segments (one lane
+// each, partials in segment order), slices are sorted by length (longest first) and
+// padded to multiples of kSellUnroll with column 0 / value 0, lanes past the units
+// hold -1.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -19,6 +20,21 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
     SellHost h;
     sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h);
     std::vector<int> seen((size_t)n_rows, 0);
+    // Segments: partial p -> (long row, first term); long_ptr gives each row's partials.
+    const int32_t n_parts = h.long_ptr.back();
+    std::vector<int> part_seen((size_t)n_parts, 0);
+    std::vector<int32_t> part_row((size_t)n_parts), part_start((size_t)n_parts);
+    for (size_t i = 0; i < h.long_rows.size(); i++) {
+        const int32_t r = h.long_rows[i];
+        if (rp[r + 1] - rp[r] <= max_len) { printf("FAIL long row\n"); return 1; }
+        if (h.long_ptr[i + 1] - h.long_ptr[i] != (rp[r + 1] - rp[r] + max_len - 1) / max_len) {
+            printf("FAIL segment count\n"); return 1; }
+        for (int32_t p = h.long_ptr[i]; p < h.long_ptr[i + 1]; p++) {
+            part_row[(size_t)p] = r;
+            part_start[(size_t)p] = rp[r] + (p - h.long_ptr[i]) * max_len;
+        }
+        seen[(size_t)r] = 1;
+    }
     int64_t slots = 0;
     int32_t prev_len = INT32_MAX;
     for (int64_t s = 0; s < h.n_slices; s++) {
@@ -28,6 +44,20 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
         for (int l = 0; l < kSellLanes; l++) {
             const int32_t r = h.row[(size_t)(s * kSellLanes + l)];
             const int32_t n = h.row_len[(size_t)(s * kSellLanes + l)];
+            if (r < -1) {   // a segment of a long row
+                const int32_t p = -2 - r;
+                if (p >= n_parts) { printf("FAIL partial index\n"); return 1; }
+                part_seen[(size_t)p]++;
+                const int32_t lr = part_row[(size_t)p], a = part_start[(size_t)p];
+                if (n != std::min(max_len, rp[lr + 1] - a) || n > L) { printf("FAIL segment length\n"); return 1; }
+                if (n > prev_len) { printf("FAIL order\n"); return 1; }
+                prev_len = n;
+                for (int32_t j = 0; j < n; j++) {
+                    const size_t k = (size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l);
+                    if (h.col[k] != col[a + j] || h.val[k] != val[a + j]) { printf("FAIL segment term\n"); return 1; }
+                }
+                continue;
+            }
             if (r < 0) {
                 if (n != 0) { printf("FAIL empty lane\n"); return 1; }
                 for (int32_t j = 0; j < L; j++)
@@ -47,10 +77,10 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
         }
     }
     if (slots != h.padded || (int64_t)h.col.size() != slots) { printf("FAIL sizes\n"); return 1; }
-    for (int64_t r = 0; r < n_rows; r++) {
-        const bool want = rp[r + 1] - rp[r] <= max_len;
-        if (seen[(size_t)r] != (want ? 1 : 0)) { printf("FAIL coverage row %lld\n", (long long)r); return 1; }
-    }
+    for (int64_t r = 0; r < n_rows; r++)
+        if (seen[(size_t)r] != 1) { printf("FAIL coverage row %lld\n", (long long)r); return 1; }
+    for (int32_t p = 0; p < n_parts; p++)
+        if (part_seen[(size_t)p] != 1) { printf("FAIL segment coverage %d\n", p); return 1; }
     return 0;
 }
 

@@ -1,8 +1,8 @@
 """Sorted sliced-ELL SpMV (sell.cpp + kernels_sell.hip) through the C ABI.
 
-Every row of at most the stream tile size is summed by one lane in stored order, so
-those rows are bit-identical to the reference's order (oracle.csr_spmv); longer rows
-run as the stream plan's chunks (tree sums) and are checked within 1e-6 * sum|terms|.
+Every row of at most 2048 terms is summed by one lane in stored order, so those rows
+are bit-identical to the reference's order (oracle.csr_spmv); longer rows are cut in
+2048-term segments whose sums are added in order, checked within 1e-6 * sum|terms|.
 """
 import numpy as np
 import pytest
@@ -60,7 +60,7 @@ def test_sell_uniform_bit_exact(sm, n_rows, n_cols, per_row):
 
 @pytest.mark.parametrize("relabel", [0, 1])
 def test_sell_skewed_rows_and_long_rows(sm, relabel):
-    """Power-law row lengths with empty rows and rows past the tile size (chunked):
+    """Power-law row lengths with empty rows and rows past 2048 terms (segmented):
     short rows bit-exact, all rows within the bound; the column relabeling (x
     permuted per SpMV) gives the same bits."""
     rng = np.random.default_rng(7)

@@ -44,7 +44,7 @@ def test_band2_builder_under_asan(tmp_path):
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
 def test_sell_builder_under_asan(tmp_path):
     """Sorted sliced-ELL builder (sell.cpp): every short row in exactly one lane with its
-    terms in stored order, slices sorted and padded, long rows left out."""
+    terms in stored order, long rows in consecutive segments, slices sorted and padded."""
     exe = tmp_path / "sell_asan"
     src = [os.path.join(ROOT, "tests", "native", "sell_asan.cpp"),
            os.path.join(ROOT, "sparsematrix_amd", "csrc", "sell.cpp")]
