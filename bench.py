@@ -98,6 +98,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
     ap.add_argument("--spmm-n", type=int, default=32)
+    ap.add_argument("--no-rmat", action="store_true",
+                    help="skip the config-4 line (R-MAT scale 24 SpMV, N = 1 only)")
+    ap.add_argument("--rmat-scale", type=int, default=24)
     ap.add_argument("--no-graph", action="store_true",
                     help="N=1: launch each timed step from Python instead of replaying the K "
                          "steps as one captured HIP graph")
@@ -288,6 +291,51 @@ def main():
                 "~2 flop/B is HBM/gather bound; see DESIGN.md)"}
         del X, Y
 
+    # ---- R-MAT (config 4) on rank 0 at N = 1: AUTO on a Graph500 graph --------------
+    rmat = None
+    if world == 1 and rank == 0 and not args.no_rmat:
+        try:   # a failure here must not cost the config-2 line
+            from sparsematrix_amd import synth
+            torch.cuda.synchronize()
+            t_b = time.perf_counter()
+            rrp, rci, rva = synth.rmat_device(args.rmat_scale, 16, seed=4)
+            rn = 1 << args.rmat_scale
+            t_g = time.perf_counter()
+            RM = smd.SparseMatrix.from_csr(rrp, rci, rva, rn, device=dev_index)
+            t_c = time.perf_counter()
+            rinfo = RM.info()
+            g = torch.Generator(device=dev).manual_seed(4)
+            rx = torch.rand(rn, generator=g, device=dev) * 2 - 1
+            ry = torch.rand(rn, generator=g, device=dev) * 2 - 1
+            for _ in range(3):
+                RM.spmv(rx, ry, 1.0, 0.5)
+            torch.cuda.synchronize()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(10)]
+            for a, b in ev:
+                a.record()
+                RM.spmv(rx, ry, 1.0, 0.5)
+                b.record()
+            torch.cuda.synchronize()
+            r_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+            rnnz = int(rci.numel())
+            rb = spmv_bytes(rnnz, rn, rn)
+            kind = ("band kind %d" % rinfo["has_xband"] if rinfo["has_xband"]
+                    else "sorted sliced-ELL + long-row segments" if rinfo["sell_slices"]
+                    else "stream")
+            rmat = {"scale": args.rmat_scale, "rows": rn, "nnz": rnnz,
+                    "max_row_nnz": rinfo["max_row_nnz"], "ms": round(r_ms, 4),
+                    "alg_bytes": rb, "gbs": round(rb / (r_ms * 1e-3) / 1e9, 1),
+                    "frac": round(rb / (r_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "kernel": kind + (", relabeled columns" if rinfo["col_relabel"] else ""),
+                    "generate_s": round(t_g - t_b, 1), "build_s": round(t_c - t_g, 1),
+                    "timing": "HIP events around each SpMV (median of 10, eager launches, "
+                              "x permutation and finalize included)"}
+            del RM, rrp, rci, rva, rx, ry
+            torch.cuda.empty_cache()
+        except Exception as exc:  # noqa: BLE001
+            rmat = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
     # ---- CPU baseline (rank 0, N = 1) --------------------------------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu:
@@ -338,7 +386,7 @@ def main():
                            ", RCCL all-gather(x)" + (" of step k+1 overlapped with SpMV k"
                                                      if overlap else "") if world > 1 else ""),
                        **({"emulate_world": emu} if emu > 1 else {})},
-            "roofline": roof, "cpu_baseline": cpu, "spmm": spmm,
+            "roofline": roof, "cpu_baseline": cpu, "spmm": spmm, "rmat": rmat,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

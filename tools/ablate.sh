@@ -12,7 +12,7 @@ cd /tmp || exit 1
 for v in ${VARIANTS:-0}; do
   export "${ABL_ENV:-SM_CTILE_ABLATE}=$v"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/v$v" -o run -- \
-      python3 "$ROOT/bench.py" --no-cpu --no-spmm --steps 20 --warmup 3 ${BENCH_ARGS:-} > "$OUT/v$v.log" 2>&1 \
+      python3 "$ROOT/bench.py" --no-cpu --no-spmm --no-rmat --steps 20 --warmup 3 ${BENCH_ARGS:-} > "$OUT/v$v.log" 2>&1 \
       || { echo "variant $v failed"; tail -20 "$OUT/v$v.log"; exit 1; }
   echo "== variant $v"
   python3 - "$OUT/v$v" <<'PY'

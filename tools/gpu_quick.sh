@@ -13,7 +13,7 @@ fi
 export TMPDIR=/tmp
 rm -rf "$OUT/qprof"
 ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/qprof" -o run -- \
-    python3 "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu --no-spmm ${BENCH_ARGS:-} ) > "$OUT/qprof.log" 2>&1 || { tail -30 "$OUT/qprof.log"; exit 14; }
+    python3 "$ROOT/bench.py" --steps 30 --warmup 5 --no-cpu --no-spmm --no-rmat ${BENCH_ARGS:-} ) > "$OUT/qprof.log" 2>&1 || { tail -30 "$OUT/qprof.log"; exit 14; }
 grep -h '^{' "$OUT/qprof.log" | tail -1 | cut -c1-400
 python3 - "$OUT/qprof" <<'PY'
 import csv, glob, sys

@@ -9,7 +9,7 @@ OUT=$ROOT/gpurun_out/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-BENCH=${PMC_CMD:-"python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu --no-spmm ${BENCH_ARGS:-}"}
+BENCH=${PMC_CMD:-"python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu --no-spmm --no-rmat ${BENCH_ARGS:-}"}
 for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   tag=$(echo "$ctr" | tr ' ' '_')
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/bench_$tag" -o run -- $BENCH > "$OUT/bench_$tag.log" 2>&1 || { tail -20 "$OUT/bench_$tag.log"; exit 21; }
