@@ -423,7 +423,6 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
     SellDev &d = p.sell;
     d.max_len = max_len;
-    d.n_cols = m->n_cols;
     d.n_long = (int32_t)sh.long_rows.size();
     const int32_t n_parts = sh.long_ptr.back();
     SM_TRY_HIP(dev_alloc(&d.d_long_rows, d.n_long, m->device_bytes));

@@ -14,7 +14,6 @@
 #include "sm_internal.h"
 #include "sell.h"
 
-#include <algorithm>
 #include <cstdlib>
 
 namespace smamd {
@@ -60,64 +59,7 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
         }
     }
     if (r >= 0) y[r] = acc;
-}
-
-// Persistent variant for relabeled columns (development A/B, SM_SELL_HOT=1): two
-// 1024-thread workgroups per CU keep x of the H hottest columns (a dense prefix after
-// the relabeling by descending degree) in LDS and walk the slices round-robin; a
-// term whose column is in the prefix reads LDS, the others gather from memory (the
-// lanes of the other kind issue a load past the descriptor: no memory request).
-template <int U, int H>
-__global__ __launch_bounds__(1024) void spmv_sell_hot_kernel(
-    int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
-    const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
-    const int32_t *__restrict__ col, const float *__restrict__ val, const float *__restrict__ x,
-    int64_t n_cols, float *__restrict__ y, float *__restrict__ partials, float alpha, float beta) {
-    __shared__ __attribute__((aligned(16))) float xh[H];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int64_t nh = n_cols < H ? n_cols : H;
-    for (int i = tid; i < H; i += 1024) xh[i] = i < nh ? x[i] : 0.0f;
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t x_src = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(x), (short)0, (int)(n_cols * 4 > 0x7FFFFFFF ? 0x7FFFFFFF : n_cols * 4),
-        0x00020000);
-    const int64_t stride = (int64_t)gridDim.x * 16;
-    for (int64_t s = (int64_t)blockIdx.x * 16 + (tid >> 6); s < n_slices; s += stride) {
-        const int64_t base = off[s];
-        const int32_t L = len[s];
-        const int32_t r = row[s * kSellLanes + lane];
-        const int32_t n = row_len[s * kSellLanes + lane];
-        float acc = r >= 0 ? y[r] : -0.0f;
-        if (r >= 0 && beta != 1.0f) acc = __fmul_rn(acc, beta);
-        const int32_t *c = col + base + lane;
-        const float *v = val + base + lane;
-        for (int32_t j = 0; j < L; j += U) {
-            int32_t cc[U];
-            float vv[U], xg[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                cc[u] = __builtin_nontemporal_load(c + (int64_t)(j + u) * kSellLanes);
-                vv[u] = __builtin_nontemporal_load(v + (int64_t)(j + u) * kSellLanes);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool hot = cc[u] < H;
-                const uint32_t o = hot ? 0xFFFFFFF0u : 4u * (uint32_t)cc[u];
-                xg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x_src, o, 0, 0));
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool hot = cc[u] < H;
-                const float xl = xh[hot ? cc[u] : 0];
-                const float xv = hot ? xl : xg[u];
-                const float t = __fmul_rn(xv, __fmul_rn(vv[u], alpha));
-                if (j + u < n) acc = __fadd_rn(acc, t);
-            }
-        }
-        if (r >= 0) y[r] = acc;
-        else if (r < -1) partials[-2 - r] = acc;
-    }
+    else if (r < -1) partials[-2 - r] = acc;
 }
 
 }  // namespace
@@ -144,24 +86,6 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         const char *e = getenv("SM_SELL_UNROLL");
         return e ? atoi(e) : 8;
     }();
-    static const bool hot = [] {
-        const char *e = getenv("SM_SELL_HOT");
-        return e && atoi(e) == 1;
-    }();
-    if (hot && sd.n_cols > 0) {
-        int dev = 0, n_cu = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-        const int64_t wgs = std::min<int64_t>(2 * (int64_t)n_cu, (sd.n_slices + 15) / 16);
-        hipLaunchKernelGGL((spmv_sell_hot_kernel<8, 16384>), dim3((unsigned)wgs), dim3(1024), 0, s,
-                           sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col,
-                           sd.d_val, x, sd.n_cols, y, sd.d_partials, alpha, beta);
-        hipError_t e = hipGetLastError();
-        return e == hipSuccess ? launch_long_finalize(sd.n_long, sd.d_long_rows, sd.d_long_ptr,
-                                                      sd.d_partials, y, beta, s)
-                               : e;
-        return hipGetLastError();
-    }
     if (abl == 1) SM_SELL_K(8, 1);
     else if (unroll == 16) SM_SELL_K(16, 0);
     else if (unroll == 32) SM_SELL_K(32, 0);

@@ -65,7 +65,6 @@ struct SellDev {
     int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
     float *d_val = nullptr;
     int32_t max_len = 0;              // rows up to this length are whole lanes
-    int64_t n_cols = 0;               // x length (the hot-prefix variant)
     // Rows longer than max_len: cut in segments (lanes with row = -2 - partial).
     int32_t n_long = 0;
     int32_t *d_long_rows = nullptr;   // n_long
