@@ -7,6 +7,7 @@
 #include "sell.h"
 
 #include <algorithm>
+#include <thread>
 
 namespace smamd {
 
@@ -54,17 +55,30 @@ void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t
     out.padded = slots;
     out.col.assign((size_t)slots, 0);
     out.val.assign((size_t)slots, 0.0f);
-    for (int64_t i = 0; i < n_units; i++) {
-        const int64_t s = i / kSellLanes, l = i % kSellLanes;
-        const Unit &u = units[(size_t)order[(size_t)i]];
-        out.row[(size_t)i] = u.part >= 0 ? -2 - u.part : u.row;
-        out.row_len[(size_t)i] = u.n;
-        int32_t *c = out.col.data() + out.off[(size_t)s] + l;
-        float *v = out.val.data() + out.off[(size_t)s] + l;
-        for (int32_t j = 0; j < u.n; j++) {
-            c[(size_t)j * kSellLanes] = col[u.start + j];
-            v[(size_t)j * kSellLanes] = val[u.start + j];
+    // Fill the slots, slices split across threads (disjoint lanes: no sharing).
+    auto fill = [&](int64_t s0, int64_t s1) {
+        for (int64_t i = s0 * kSellLanes; i < std::min(n_units, s1 * kSellLanes); i++) {
+            const int64_t s = i / kSellLanes, l = i % kSellLanes;
+            const Unit &u = units[(size_t)order[(size_t)i]];
+            out.row[(size_t)i] = u.part >= 0 ? -2 - u.part : u.row;
+            out.row_len[(size_t)i] = u.n;
+            int32_t *c = out.col.data() + out.off[(size_t)s] + l;
+            float *v = out.val.data() + out.off[(size_t)s] + l;
+            for (int32_t j = 0; j < u.n; j++) {
+                c[(size_t)j * kSellLanes] = col[u.start + j];
+                v[(size_t)j * kSellLanes] = val[u.start + j];
+            }
         }
+    };
+    const int nthr = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nthr == 1 || slots < (1 << 20)) {
+        fill(0, out.n_slices);
+    } else {
+        std::vector<std::thread> th;
+        const int64_t per = (out.n_slices + nthr - 1) / nthr;
+        for (int t = 0; t < nthr; t++)
+            th.emplace_back(fill, std::min(out.n_slices, t * per), std::min(out.n_slices, (t + 1) * per));
+        for (auto &x : th) x.join();
     }
 }
 

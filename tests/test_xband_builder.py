@@ -50,7 +50,7 @@ def test_sell_builder_under_asan(tmp_path):
            os.path.join(ROOT, "sparsematrix_amd", "csrc", "sell.cpp")]
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
                     "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
-                    *src, "-o", str(exe)], check=True)
+                    *src, "-o", str(exe), "-pthread"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
