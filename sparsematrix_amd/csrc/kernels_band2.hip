@@ -57,6 +57,9 @@ constexpr int kB2Threads = 1024;
 #ifndef SM_CB_TAB_COPIES
 #define SM_CB_TAB_COPIES 32
 #endif
+#ifndef SM_E_EARLY
+#define SM_E_EARLY 0
+#endif
 #ifndef SM_X_AUX
 #define SM_X_AUX 0
 #endif
@@ -100,8 +103,13 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // the loads need no more cover, and more of them in flight only slow the rest.
     constexpr int AX = CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
     constexpr int AE = CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
-    constexpr int U = AX > AE ? AX : AE;   // loop unroll: both rings' roles static
-    static_assert(U % AX == 0 && U % AE == 0 && U % 2 == 0, "ring sizes divide the unroll");
+    // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
+    // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
+    constexpr bool kEarly = SM_E_EARLY != 0;
+    constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
+    constexpr int U0 = AX > ER ? AX : ER;
+    constexpr int U = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
+    static_assert(U % AX == 0 && U % ER == 0 && U % 2 == 0, "ring sizes divide the unroll");
     static_assert(W % 4 == 0 && XV * 4 * kB2Threads >= W, "float4 slots cover the window");
     __shared__ __attribute__((aligned(16))) float xs[2][W];
     // Wide band2: + a scratch slot per lane (dummy lanes write there).  The other
@@ -347,11 +355,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // Prologue = virtual bands -U..-1 (their loads in the loop's order), so the loads
     // pending at the loop header are in the order the loop's back edge leaves them.
     float4 X[AX][XV];
-    EV E[AE];
+    EV E[ER];
 #pragma unroll
     for (int v = -U; v < 0; ++v) {
         if (v + AX >= 0) load_x(v + AX, X[v + AX]);
-        if (v + AE >= 0) E[v + AE] = load_e(v + AE);
+        if (v + AE >= 0) E[(v + AE) % ER] = load_e(v + AE);
     }
     store_x(0, X[0]);
     __syncthreads();
@@ -370,14 +378,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if (q + AX >= cw + 64) advance();
             load_x(q + AX, X[u % AX]);
             store_x((u + 1) & 1, X[(u + 1) % AX]);
+            if constexpr (kEarly) E[(u + AE) % ER] = load_e(q + AE);
             if constexpr (ABL & 1) {
-                asm volatile("" ::"v"(E[u % AE].x), "v"(E[u % AE].y));
+                asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
             } else if constexpr (CB) {
-                apply_cb(xs[u & 1], E[u % AE]);
+                apply_cb(xs[u & 1], E[u % ER]);
             } else {
-                apply_b2(xs[u & 1], E[u % AE]);
+                apply_b2(xs[u & 1], E[u % ER]);
             }
-            E[u % AE] = load_e(q + AE);
+            if constexpr (!kEarly) E[u % ER] = load_e(q + AE);
             if (!(ABL & 512) && q < nb) __syncthreads();
         }
     }
