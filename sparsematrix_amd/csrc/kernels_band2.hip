@@ -57,6 +57,14 @@ constexpr int kB2Threads = 1024;
 #ifndef SM_CB_TAB_COPIES
 #define SM_CB_TAB_COPIES 32
 #endif
+// SM_CB_DMA (development A/B, wide cband): x windows go L2 -> LDS by LDS-DMA one
+// band ahead (no register ring), entries SM_CB_DMA_EAHEAD bands ahead.
+#ifndef SM_CB_DMA
+#define SM_CB_DMA 0
+#endif
+#ifndef SM_CB_DMA_EAHEAD
+#define SM_CB_DMA_EAHEAD 4
+#endif
 #ifndef SM_E_EARLY
 #define SM_E_EARLY 0
 #endif
@@ -101,8 +109,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // (loaded AX-1 bands ago) retires every older load.  Measured (config 2): a
     // lookahead of 2 bands beats 6 (38.3 vs 40.6 us cband, 38.3 vs 41.5 band2) --
     // the loads need no more cover, and more of them in flight only slow the rest.
-    constexpr int AX = CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
-    constexpr int AE = CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
+    // kDma: window q+1 is LDS-DMA'd at band q into the buffer band q-1 read; hipcc
+    // does not count the (asm) DMA, so its own wait for the entries of band q counts
+    // only the AE-1 younger entry loads -- at least the 3 ops really pending then
+    // (one entry load, the window's two DMA pieces) once AE >= 4: no extra stall.
+    constexpr bool kDma = CB && !TALL && SM_CB_DMA != 0;
+    static_assert(!kDma || SM_CB_DMA_EAHEAD >= 4, "DMA variant: hipcc's entry waits must not stall");
+    constexpr int AX = kDma ? 1 : CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
+    constexpr int AE = kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
     // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
     // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
     constexpr bool kEarly = SM_E_EARLY != 0;
@@ -167,6 +181,26 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if (!(ABL & 2)) v = __builtin_amdgcn_raw_buffer_load_b128(x_src, off, 0, SM_X_AUX);
             xr[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                                 __uint_as_float(v.w));
+        }
+    };
+    // kDma: piece m (256 floats, 1 KiB) of window q is wave-instruction k of wave
+    // m % 16; windows past the tile land zeros in a buffer nobody reads any more.
+    const uint32_t xs_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) float *)&xs[0][0];
+    auto dma_x = [&](int32_t q, int buf) {
+        const int32_t c = q < nb ? clo_at(q) : 0;
+#pragma unroll
+        for (int k = 0; k < XV; ++k) {
+            const int32_t m = k * (kB2Threads / 64) + (tid >> 6);
+            const uint32_t voff =
+                q < nb && !(ABL & 2) ? 4u * (uint32_t)(c + m * 256 + lane * 4) : 0xFFFFFFF0u;
+            const uint32_t lds = __builtin_amdgcn_readfirstlane(xs_lds + 4u * (uint32_t)(buf * W + m * 256));
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(x_src), "s"(lds)
+                : "memory");
         }
     };
     auto store_x = [&](int buf, const float4 *xr) {
@@ -356,12 +390,19 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // pending at the loop header are in the order the loop's back edge leaves them.
     float4 X[AX][XV];
     EV E[ER];
+    if constexpr (kDma) {
 #pragma unroll
-    for (int v = -U; v < 0; ++v) {
-        if (v + AX >= 0) load_x(v + AX, X[v + AX]);
-        if (v + AE >= 0) E[(v + AE) % ER] = load_e(v + AE);
+        for (int v = 0; v < AE; ++v) E[v] = load_e(v);
+        dma_x(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+#pragma unroll
+        for (int v = -U; v < 0; ++v) {
+            if (v + AX >= 0) load_x(v + AX, X[v + AX]);
+            if (v + AE >= 0) E[(v + AE) % ER] = load_e(v + AE);
+        }
+        store_x(0, X[0]);
     }
-    store_x(0, X[0]);
     __syncthreads();
 
     // Whole groups of U bands (static ring indices, no branch around a load or a
@@ -376,8 +417,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
             if (q + AX >= cw + 64) advance();
-            load_x(q + AX, X[u % AX]);
-            store_x((u + 1) & 1, X[(u + 1) % AX]);
+            if constexpr (kDma) {
+                dma_x(q + 1, (u + 1) & 1);
+            } else {
+                load_x(q + AX, X[u % AX]);
+                store_x((u + 1) & 1, X[(u + 1) % AX]);
+            }
             if constexpr (kEarly) E[(u + AE) % ER] = load_e(q + AE);
             if constexpr (ABL & 1) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
@@ -387,6 +432,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 apply_b2(xs[u & 1], E[u % ER]);
             }
             if constexpr (!kEarly) E[u % ER] = load_e(q + AE);
+            // kDma: window q+1 landed (in-order retirement); the entry load just issued flies.
+            if constexpr (kDma) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
             if (!(ABL & 512) && q < nb) __syncthreads();
         }
     }
