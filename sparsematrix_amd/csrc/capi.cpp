@@ -416,8 +416,14 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     // longer ones as max_len-term segments.  SM_SELL_MAX overrides the cap.
     int32_t max_len = kSellMaxLen;
     if (const char *e = getenv("SM_SELL_MAX")) max_len = std::max(1, atoi(e));
+    // SM_SELL_SIGMA: sort within windows of that many rows (0: one window),
+    // SM_SELL_STREAMS: XCD streams of windows (default 8 with windows).
+    int64_t sigma = 0;
+    if (const char *e = getenv("SM_SELL_SIGMA")) sigma = std::max<int64_t>(0, atoll(e));
+    int streams = sigma > 0 ? 8 : 1;
+    if (const char *e = getenv("SM_SELL_STREAMS")) streams = std::max(1, atoi(e));
     SellHost sh;
-    sell_build(rp, c, val, m->n_rows, max_len, sh);
+    sell_build(rp, c, val, m->n_rows, max_len, sh, sigma, streams);
     std::vector<int32_t>().swap(rcol);
     if (sh.n_slices == 0) return SM_OK;
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;

@@ -19,7 +19,7 @@
 namespace smamd {
 namespace {
 
-constexpr int kSellThreads = 256;
+constexpr int kSellThreads = 64 * kSellGroup;
 
 // ABL (development only, SM_SELL_ABLATE; results wrong): 1 replaces the x gathers by
 // one broadcast address.

@@ -10,6 +10,7 @@ namespace smamd {
 constexpr int kSellLanes = 64;    // rows per slice: one wavefront
 constexpr int kSellUnroll = 8;    // slice lengths are padded to a multiple of this
 constexpr int kSellMaxLen = 2048;  // longer rows are cut in segments of this many terms
+constexpr int kSellGroup = 4;     // slices per 256-thread workgroup (kernels_sell.hip)
 
 // Rows of at most `max_len` terms, and segments of max_len terms of the longer rows,
 // sorted by length (longest first, ties in row / segment order), cut into slices of
@@ -31,8 +32,15 @@ struct SellHost {
     std::vector<int32_t> long_ptr;      // long_rows.size() + 1: their partials
 };
 
-// col: the matrix's (possibly relabeled) columns.
+// col: the matrix's (possibly relabeled) columns.  sigma > 0: rows are sorted only
+// within windows of sigma rows (SELL-C-sigma; slices never cross a window), so the
+// y entries a window's slices read and write stay few; streams > 1: the windows are
+// dealt round-robin to `streams` streams and the slices ordered so that workgroup b
+// (kSellGroup slices) takes group b / streams of stream b % streams -- with
+// workgroups dealt round-robin over the XCDs, a window's y lines stay in one XCD's
+// L2 (speed only).  Streams are padded to whole, equal numbers of groups with empty
+// slices (length 0, every lane -1).
 void sell_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                int32_t max_len, SellHost &out);
+                int32_t max_len, SellHost &out, int64_t sigma = 0, int streams = 1);
 
 }  // namespace smamd

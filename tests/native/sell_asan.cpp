@@ -2,8 +2,9 @@
 // built with AddressSanitizer by tests/test_xband_builder.py.  For random and skewed
 // shapes: every row of at most max_len terms sits in exactly one lane with its terms
 // in stored order, every longer row in consecutive max_len-term segments (one lane
-// each, partials in segment order), slices are sorted by length (longest first) and
-// padded to multiples of kSellUnroll with column 0 / value 0, lanes past the units
+// each, partials in segment order), slices are sorted by length (longest first; with
+// sigma windows: within a slice, whose units share one window, dealt to the stream of
+// the slice's group) and padded to multiples of kSellUnroll with column 0 / value 0, lanes past the units
 // hold -1.
 #include <algorithm>
 #include <cmath>
@@ -16,9 +17,10 @@
 using namespace smamd;
 
 static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
-                 const std::vector<float> &val, int64_t n_rows, int32_t max_len) {
+                 const std::vector<float> &val, int64_t n_rows, int32_t max_len,
+                 int64_t sigma = 0, int streams = 1) {
     SellHost h;
-    sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h);
+    sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h, sigma, streams);
     std::vector<int> seen((size_t)n_rows, 0);
     // Segments: partial p -> (long row, first term); long_ptr gives each row's partials.
     const int32_t n_parts = h.long_ptr.back();
@@ -39,6 +41,13 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
     int32_t prev_len = INT32_MAX;
     for (int64_t s = 0; s < h.n_slices; s++) {
         const int32_t L = h.len[(size_t)s];
+        if (sigma > 0) prev_len = INT32_MAX;   // sorted within windows: order per slice
+        int64_t slice_win = -1;               // every unit of a slice in one window
+        auto same_window = [&](int32_t row) {   // ... and in the stream its group belongs to
+            if (sigma <= 0) return true;
+            if (slice_win < 0) slice_win = row / sigma;
+            return row / sigma == slice_win && slice_win % streams == (s / kSellGroup) % streams;
+        };
         if (h.off[(size_t)s] != slots || L % kSellUnroll) { printf("FAIL slice offsets\n"); return 1; }
         slots += (int64_t)L * kSellLanes;
         for (int l = 0; l < kSellLanes; l++) {
@@ -50,7 +59,7 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
                 part_seen[(size_t)p]++;
                 const int32_t lr = part_row[(size_t)p], a = part_start[(size_t)p];
                 if (n != std::min(max_len, rp[lr + 1] - a) || n > L) { printf("FAIL segment length\n"); return 1; }
-                if (n > prev_len) { printf("FAIL order\n"); return 1; }
+                if (n > prev_len || !same_window(lr)) { printf("FAIL order\n"); return 1; }
                 prev_len = n;
                 for (int32_t j = 0; j < n; j++) {
                     const size_t k = (size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l);
@@ -65,7 +74,7 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
                 continue;
             }
             if (r >= n_rows || n != rp[r + 1] - rp[r] || n > max_len || n > L) { printf("FAIL row\n"); return 1; }
-            if (n > prev_len) { printf("FAIL order\n"); return 1; }
+            if (n > prev_len || !same_window(r)) { printf("FAIL order\n"); return 1; }
             prev_len = n;
             seen[(size_t)r]++;
             for (int32_t j = 0; j < L; j++) {
@@ -97,7 +106,12 @@ int main() {
                 for (int32_t j = 0; j < n; j++) { col.push_back((int32_t)(rng() % 100000)); val.push_back((float)(rng() % 97) - 48.0f); }
                 rp[(size_t)r + 1] = (int32_t)col.size();
             }
-            for (int32_t mx : {1, 16, 2048}) bad += check(rp, col, val, n_rows, mx);
+            for (int32_t mx : {1, 16, 2048}) {
+                bad += check(rp, col, val, n_rows, mx);
+                bad += check(rp, col, val, n_rows, mx, 1000, 1);
+                bad += check(rp, col, val, n_rows, mx, 4096, 8);
+                bad += check(rp, col, val, n_rows, mx, 64, 3);
+            }
         }
     }
     printf(bad ? "sell_asan: FAILED\n" : "sell_asan: ok\n");
