@@ -77,6 +77,23 @@ def test_sell_skewed_rows_and_long_rows(sm, relabel):
         _check(M, rp, ci, va, x, y0, alpha, beta, exact_max=2048)
 
 
+@pytest.mark.parametrize("sigma,streams", [(4096, 8), (4096, 1), (1000, 3)])
+def test_sell_sort_windows(sm, sigma, streams):
+    """SELL-C-sigma layouts (SM_SELL_SIGMA rows per sort window, SM_SELL_STREAMS XCD
+    streams of windows): the same per-row order, so the same bits as one window."""
+    rng = np.random.default_rng(11)
+    n_rows, n_cols = 30011, 40000
+    lengths = np.minimum((rng.pareto(1.1, n_rows) * 4).astype(np.int64), 6000)
+    lengths[::5] = 0
+    rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=12)
+    M, _ = with_env("SM_SELL_SIGMA", str(sigma), lambda: with_env(
+        "SM_SELL_STREAMS", str(streams), lambda: _sell(sm, rp, ci, va, n_cols, 0)))
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    for alpha, beta in ((1.0, 1.0), (1.3, 0.0)):
+        _check(M, rp, ci, va, x, y0, alpha, beta, exact_max=2048)
+
+
 def test_sell_special_values(sm):
     n_rows, n_cols = 20000, 30000
     rp, ci, va = uniform_csr(n_rows, n_cols, 9, seed=3)
