@@ -321,8 +321,9 @@ def main():
             rnnz = int(rci.numel())
             rb = spmv_bytes(rnnz, rn, rn)
             kind = ("band kind %d" % rinfo["has_xband"] if rinfo["has_xband"]
-                    else "sorted sliced-ELL + long-row segments" if rinfo["sell_slices"]
-                    else "stream")
+                    else ("sorted sliced-ELL (%s) + long-row segments"
+                          % ("4-byte column|codebook-id words" if rinfo["sell_codebook"] else "column + value")
+                          if rinfo["sell_slices"] else "stream"))
             rmat = {"scale": args.rmat_scale, "rows": rn, "nnz": rnnz,
                     "max_row_nnz": rinfo["max_row_nnz"], "ms": round(r_ms, 4),
                     "alg_bytes": rb, "gbs": round(rb / (r_ms * 1e-3) / 1e9, 1),

@@ -109,6 +109,8 @@ typedef struct sm_info {
                                    relabeling by descending degree (skewed graphs) */
     int32_t xband_slab_cols;    /* columns per slab (slab s = [s*c, (s+1)*c))   */
     int64_t sell_slices;        /* sorted sliced-ELL slices of 64 rows (0: not built) */
+    int32_t sell_codebook;      /* 1: the slices hold 4-byte column | codebook-id words */
+    int32_t reserved0;
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */

@@ -53,7 +53,7 @@ class SmInfo(C.Structure):
         ("max_row_nnz", C.c_int32), ("has_xband", C.c_int32), ("xband_blocks", C.c_int32),
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
-        ("sell_slices", C.c_int64),
+        ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("reserved0", C.c_int32),
     ]
 
 

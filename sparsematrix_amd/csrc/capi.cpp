@@ -96,6 +96,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.sell.d_row_len);
     (void)hipFree(m->plan.sell.d_col);
     (void)hipFree(m->plan.sell.d_val);
+    (void)hipFree(m->plan.sell.d_table);
     (void)hipFree(m->plan.sell.d_long_rows);
     (void)hipFree(m->plan.sell.d_long_ptr);
     (void)hipFree(m->plan.sell.d_partials);
@@ -422,9 +423,18 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     if (const char *e = getenv("SM_SELL_SIGMA")) sigma = std::max<int64_t>(0, atoll(e));
     int streams = sigma > 0 ? 8 : 1;
     if (const char *e = getenv("SM_SELL_STREAMS")) streams = std::max(1, atoi(e));
+    // Codebook form (SM_SELL_CB=0 disables it): values of <= 255 distinct bit patterns
+    // and columns < 2^24 -- one 4-byte word per slot instead of column + value.
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    const char *ecb = getenv("SM_SELL_CB");
+    const bool cb = !(ecb && atoi(ecb) == 0) && m->n_cols <= ((int64_t)1 << kSellCbColBits) &&
+                    codebook_ids(val, m->nnz, table, ids);
+    if (!cb) std::vector<uint8_t>().swap(ids);
     SellHost sh;
-    sell_build(rp, c, val, m->n_rows, max_len, sh, sigma, streams);
+    sell_build(rp, c, val, m->n_rows, max_len, sh, sigma, streams, cb ? ids.data() : nullptr);
     std::vector<int32_t>().swap(rcol);
+    std::vector<uint8_t>().swap(ids);
     if (sh.n_slices == 0) return SM_OK;
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
     SellDev &d = p.sell;
@@ -445,16 +455,23 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     // + a zeroed tail of 32 slots per lane: unrolls past kSellUnroll read up to it.
     const int64_t tail = 32 * kSellLanes;
     SM_TRY_HIP(dev_alloc(&d.d_col, sh.padded + tail, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_val, sh.padded + tail, m->device_bytes));
     SM_TRY_HIP(hipMemset(d.d_col + sh.padded, 0, (size_t)tail * 4));
-    SM_TRY_HIP(hipMemset(d.d_val + sh.padded, 0, (size_t)tail * 4));
+    if (cb) {
+        SM_TRY_HIP(dev_alloc(&d.d_table, std::max<int64_t>((int64_t)table.size(), 1), m->device_bytes));
+        if (!table.empty())
+            SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+        d.table_size = (int32_t)table.size();
+    } else {
+        SM_TRY_HIP(dev_alloc(&d.d_val, sh.padded + tail, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_val + sh.padded, 0, (size_t)tail * 4));
+    }
     SM_TRY_HIP(hipMemcpy(d.d_off, sh.off.data(), sh.off.size() * 8, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_len, sh.len.data(), sh.len.size() * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_row, sh.row.data(), sh.row.size() * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_row_len, sh.row_len.data(), sh.row_len.size() * 4, hipMemcpyHostToDevice));
     if (sh.padded) {
         SM_TRY_HIP(hipMemcpy(d.d_col, sh.col.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(d.d_val, sh.val.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
+        if (!cb) SM_TRY_HIP(hipMemcpy(d.d_val, sh.val.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
     }
     d.n_slices = sh.n_slices;
     return SM_OK;
@@ -881,6 +898,7 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;
+    info->sell_codebook = m->plan.sell.d_table != nullptr;
     return SM_OK;
 }
 

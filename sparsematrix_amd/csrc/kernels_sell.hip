@@ -10,7 +10,7 @@
 // not added.  Longer rows are cut in kSellMaxLen-term segments that sit in the slices
 // like rows; each segment's sum (from -0.0) goes to a partial, and the finalize adds
 // beta * y and the partials in segment order (deterministic, within the Sum|terms|
-// bound).
+// bound).  The codebook form (spmv_csell_kernel) reads one 4-byte word per slot.
 #include "sm_internal.h"
 #include "sell.h"
 
@@ -62,13 +62,66 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
     else if (r < -1) partials[-2 - r] = acc;
 }
 
+// Codebook form (sell.h, SM_SELL_CB): slot = column | id << 24, one coalesced 256-byte
+// load per slot of 64 lanes instead of two.  The workgroup first puts fl(table[id] *
+// alpha) in LDS (kTabCopies copies, lane l reads copy l % kTabCopies: fewer bank
+// conflicts), so each term is x * fl(v * alpha) -- the same bits as the plain form.
+constexpr int kCsellTabCopies = 4;
+template <int U>
+__global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
+    int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+    const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
+    const uint32_t *__restrict__ word, const float *__restrict__ table, int32_t table_size,
+    const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials, float alpha,
+    float beta) {
+    static_assert(256 * kCsellTabCopies == 4 * kSellThreads, "one float4 of copies per thread");
+    __shared__ __attribute__((aligned(16))) float tab[256 * kCsellTabCopies];
+    {
+        const int id = threadIdx.x;   // 256 threads: one id each, all its copies
+        const float t = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
+        *reinterpret_cast<float4 *>(&tab[kCsellTabCopies * id]) = make_float4(t, t, t, t);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * (kSellThreads / 64) + (threadIdx.x >> 6);
+    if (s >= n_slices) return;   // wave-uniform, after the only barrier
+    const int64_t base = off[s];
+    const int32_t L = len[s];
+    const int32_t r = row[s * kSellLanes + lane];
+    const int32_t n = row_len[s * kSellLanes + lane];
+    float acc = r >= 0 ? y[r] : -0.0f;
+    if (r >= 0 && beta != 1.0f) acc = __fmul_rn(acc, beta);
+    const uint32_t *w = word + base + lane;
+    const int cp = lane & (kCsellTabCopies - 1);
+    constexpr uint32_t kColMask = (1u << kSellCbColBits) - 1u;
+    for (int32_t j = 0; j < L; j += U) {
+        uint32_t ww[U];
+        float xg[U], tv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ww[u] = __builtin_nontemporal_load(w + (int64_t)(j + u) * kSellLanes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            xg[u] = x[ww[u] & kColMask];
+            tv[u] = tab[(ww[u] >> kSellCbColBits) * kCsellTabCopies + cp];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float t = __fmul_rn(xg[u], tv[u]);
+            if (j + u < n) acc = __fadd_rn(acc, t);
+        }
+    }
+    if (r >= 0) y[r] = acc;
+    else if (r < -1) partials[-2 - r] = acc;
+}
+
 }  // namespace
 
 hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float alpha, float beta,
                             hipStream_t s) {
     if (sd.n_slices <= 0) return hipSuccess;
-    if (!sd.d_off || !sd.d_len || !sd.d_row || !sd.d_row_len || !sd.d_col || !sd.d_val)
+    if (!sd.d_off || !sd.d_len || !sd.d_row || !sd.d_row_len || !sd.d_col || (!sd.d_val && !sd.d_table))
         return hipErrorInvalidValue;
+    if (sd.d_table && (sd.table_size < 0 || sd.table_size > 256)) return hipErrorInvalidValue;
     const int64_t grid = (sd.n_slices + kSellThreads / 64 - 1) / (kSellThreads / 64);
     if (grid > 0x7FFFFFFF) return hipErrorInvalidValue;
     static_assert(kSellUnroll % 8 == 0, "slice lengths are multiples of the unroll");
@@ -86,7 +139,12 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         const char *e = getenv("SM_SELL_UNROLL");
         return e ? atoi(e) : 8;
     }();
-    if (abl == 1) SM_SELL_K(8, 1);
+    if (sd.d_table) {
+        hipLaunchKernelGGL((spmv_csell_kernel<8>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
+                           sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
+                           reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size,
+                           x, y, sd.d_partials, alpha, beta);
+    } else if (abl == 1) SM_SELL_K(8, 1);
     else if (unroll == 16) SM_SELL_K(16, 0);
     else if (unroll == 32) SM_SELL_K(32, 0);
     else SM_SELL_K(8, 0);

@@ -12,7 +12,7 @@
 namespace smamd {
 
 void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                int32_t max_len, SellHost &out, int64_t sigma, int streams) {
+                int32_t max_len, SellHost &out, int64_t sigma, int streams, const uint8_t *ids) {
     out = SellHost();
     // Units: a row of <= max_len terms, or one segment of a longer row.
     struct Unit {
@@ -84,7 +84,7 @@ void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t
     }
     out.padded = slots;
     out.col.assign((size_t)slots, 0);
-    out.val.assign((size_t)slots, 0.0f);
+    if (!ids) out.val.assign((size_t)slots, 0.0f);
     // Fill the slots, slices split across threads (disjoint lanes: no sharing).
     auto fill = [&](int64_t s0, int64_t s1) {
         for (int64_t s = s0; s < s1; s++) {
@@ -95,6 +95,12 @@ void sell_build(const int32_t *rp, const int32_t *col, const float *val, int64_t
                 out.row[i] = u.part >= 0 ? -2 - u.part : u.row;
                 out.row_len[i] = u.n;
                 int32_t *c = out.col.data() + out.off[(size_t)s] + l;
+                if (ids) {
+                    for (int32_t j = 0; j < u.n; j++)
+                        c[(size_t)j * kSellLanes] =
+                            (int32_t)((uint32_t)col[u.start + j] | (uint32_t)ids[u.start + j] << kSellCbColBits);
+                    continue;
+                }
                 float *v = out.val.data() + out.off[(size_t)s] + l;
                 for (int32_t j = 0; j < u.n; j++) {
                     c[(size_t)j * kSellLanes] = col[u.start + j];

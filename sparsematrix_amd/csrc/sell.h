@@ -26,8 +26,8 @@ struct SellHost {
     std::vector<int32_t> len;           // n_slices: padded slice length (multiple of kSellUnroll)
     std::vector<int32_t> row;           // n_slices * 64: original row of each lane, -1 = none
     std::vector<int32_t> row_len;       // n_slices * 64: that row's length
-    std::vector<int32_t> col;           // padded slots
-    std::vector<float> val;
+    std::vector<int32_t> col;           // padded slots (codebook: words, see below)
+    std::vector<float> val;             // padded slots (empty with codebook ids)
     std::vector<int32_t> long_rows;     // rows split in segments
     std::vector<int32_t> long_ptr;      // long_rows.size() + 1: their partials
 };
@@ -39,8 +39,13 @@ struct SellHost {
 // (kSellGroup slices) takes group b / streams of stream b % streams -- with
 // workgroups dealt round-robin over the XCDs, a window's y lines stay in one XCD's
 // L2 (speed only).  Streams are padded to whole, equal numbers of groups with empty
-// slices (length 0, every lane -1).
+// slices (length 0, every lane -1).  ids != nullptr (codebook sell, every column <
+// 2^24): each slot is one word, column | id << 24 (the value's codebook id, as the
+// reference stores it: sparse-matrix.h:46-52), and `val` stays empty -- 4 bytes per
+// slot instead of 8; padding words are 0 (never added).
+constexpr int kSellCbColBits = 24;
 void sell_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
-                int32_t max_len, SellHost &out, int64_t sigma = 0, int streams = 1);
+                int32_t max_len, SellHost &out, int64_t sigma = 0, int streams = 1,
+                const uint8_t *ids = nullptr);
 
 }  // namespace smamd

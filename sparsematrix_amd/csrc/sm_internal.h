@@ -63,7 +63,10 @@ struct SellDev {
     int32_t *d_row = nullptr;         // n_slices * 64 (-1: no row)
     int32_t *d_row_len = nullptr;     // n_slices * 64
     int32_t *d_col = nullptr;         // padded slots (relabeled columns when n_relabel > 0)
-    float *d_val = nullptr;
+    float *d_val = nullptr;           // nullptr in the codebook form
+    // Codebook form (sell.h): d_col holds column | id << 24 words, values in d_table.
+    float *d_table = nullptr;         // table_size fp32 values (nullptr: plain form)
+    int32_t table_size = 0;
     int32_t max_len = 0;              // rows up to this length are whole lanes
     // Rows longer than max_len: cut in segments (lanes with row = -2 - partial).
     int32_t n_long = 0;

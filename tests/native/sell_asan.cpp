@@ -5,7 +5,7 @@
 // each, partials in segment order), slices are sorted by length (longest first; with
 // sigma windows: within a slice, whose units share one window, dealt to the stream of
 // the slice's group) and padded to multiples of kSellUnroll with column 0 / value 0, lanes past the units
-// hold -1.
+// hold -1.  Codebook form (ids): every slot is column | id << 24, padding 0, no values.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -18,9 +18,18 @@ using namespace smamd;
 
 static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
                  const std::vector<float> &val, int64_t n_rows, int32_t max_len,
-                 int64_t sigma = 0, int streams = 1) {
+                 int64_t sigma = 0, int streams = 1, bool cb = false) {
     SellHost h;
-    sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h, sigma, streams);
+    std::vector<uint8_t> ids(val.size());
+    for (size_t i = 0; i < val.size(); i++) ids[i] = (uint8_t)(val[i] + 48.0f);   // values in [-48, 48]
+    sell_build(rp.data(), col.data(), val.data(), n_rows, max_len, h, sigma, streams,
+               cb ? ids.data() : nullptr);
+    if (cb ? !h.val.empty() : h.val.size() != h.col.size()) { printf("FAIL value slots\n"); return 1; }
+    // term i as stored: (column, value) or the codebook word with value 0
+    auto same = [&](size_t k, int64_t i) {
+        if (cb) return (uint32_t)h.col[k] == (i < 0 ? 0u : ((uint32_t)col[(size_t)i] | (uint32_t)ids[(size_t)i] << kSellCbColBits));
+        return h.col[k] == (i < 0 ? 0 : col[(size_t)i]) && h.val[k] == (i < 0 ? 0.0f : val[(size_t)i]);
+    };
     std::vector<int> seen((size_t)n_rows, 0);
     // Segments: partial p -> (long row, first term); long_ptr gives each row's partials.
     const int32_t n_parts = h.long_ptr.back();
@@ -63,7 +72,7 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
                 prev_len = n;
                 for (int32_t j = 0; j < n; j++) {
                     const size_t k = (size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l);
-                    if (h.col[k] != col[a + j] || h.val[k] != val[a + j]) { printf("FAIL segment term\n"); return 1; }
+                    if (!same(k, a + j)) { printf("FAIL segment term\n"); return 1; }
                 }
                 continue;
             }
@@ -79,9 +88,7 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
             seen[(size_t)r]++;
             for (int32_t j = 0; j < L; j++) {
                 const size_t k = (size_t)(h.off[(size_t)s] + (int64_t)j * kSellLanes + l);
-                const int32_t c = j < n ? col[rp[r] + j] : 0;
-                const float v = j < n ? val[rp[r] + j] : 0.0f;
-                if (h.col[k] != c || h.val[k] != v) { printf("FAIL term\n"); return 1; }
+                if (!same(k, j < n ? (int64_t)rp[r] + j : -1)) { printf("FAIL term\n"); return 1; }
             }
         }
     }
@@ -111,6 +118,8 @@ int main() {
                 bad += check(rp, col, val, n_rows, mx, 1000, 1);
                 bad += check(rp, col, val, n_rows, mx, 4096, 8);
                 bad += check(rp, col, val, n_rows, mx, 64, 3);
+                bad += check(rp, col, val, n_rows, mx, 0, 1, true);
+                bad += check(rp, col, val, n_rows, mx, 1000, 8, true);
             }
         }
     }

@@ -111,14 +111,16 @@ def test_header_and_python_mirror_agree():
         m = re.search(r"SM_ALGO_%s\s*=\s*(\d+)" % name.upper(), hdr)
         assert m and int(m.group(1)) == val, name
     src = ('#include <stddef.h>\n#include <stdio.h>\n#include "sparsematrix.h"\n'
-           'int main(void){printf("%zu %zu\\n", sizeof(sm_info), offsetof(sm_info, sell_slices));'
+           'int main(void){printf("%zu %zu %zu\\n", sizeof(sm_info), offsetof(sm_info, sell_slices),'
+           ' offsetof(sm_info, sell_codebook));'
            'return 0;}\n')
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
         open(c, "w").write(src)
         exe = os.path.join(d, "t")
         subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
-        size, off = map(int, subprocess.run([exe], capture_output=True, text=True,
-                                            check=True).stdout.split())
+        size, off, off_cb = map(int, subprocess.run([exe], capture_output=True, text=True,
+                                                    check=True).stdout.split())
     assert ctypes.sizeof(_lib.SmInfo) == size
     assert _lib.SmInfo.sell_slices.offset == off
+    assert _lib.SmInfo.sell_codebook.offset == off_cb

@@ -49,7 +49,8 @@ def _check(M, rp, ci, va, x, y0, alpha, beta, algo="auto", exact_max=None):
                                                    (64, 1000, 7), (65, 70, 64), (1, 10, 3)])
 def test_sell_uniform_bit_exact(sm, n_rows, n_cols, per_row):
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows)
-    M, _ = _sell(sm, rp, ci, va, n_cols)
+    M, info = _sell(sm, rp, ci, va, n_cols)
+    assert info["sell_codebook"] == 1, info   # table values: the 4-byte word form
     rng = np.random.default_rng(1)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
@@ -75,6 +76,43 @@ def test_sell_skewed_rows_and_long_rows(sm, relabel):
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (0.5, 0.0)):
         _check(M, rp, ci, va, x, y0, alpha, beta, exact_max=2048)
+
+
+@pytest.mark.parametrize("skewed", [False, True])
+def test_sell_codebook_form(sm, skewed):
+    """Values from a <= 255-entry table (the reference's uint8 ids, inf / NaN / -0.0
+    among them): the slices hold column | id << 24 words (sell_codebook = 1) and give
+    the same bits as the plain column + value form (SM_SELL_CB=0) and the oracle."""
+    rng = np.random.default_rng(21)
+    n_rows, n_cols = 40009, 70001
+    if skewed:
+        lengths = np.minimum((rng.pareto(1.1, n_rows) * 4).astype(np.int64), 7000)
+        lengths[::6] = 0
+        rp, ci, _ = skewed_csr(n_rows, n_cols, lengths, seed=22)
+    else:
+        rp, ci, _ = uniform_csr(n_rows, n_cols, 11, seed=23)
+    table = rng.uniform(-2, 2, 200).astype(np.float32)
+    table[:4] = [np.inf, np.nan, -0.0, 0.0]
+    va = table[rng.integers(0, table.size, ci.size)]
+    M, info = _sell(sm, rp, ci, va, n_cols, 0)
+    assert info["sell_codebook"] == 1, info
+    P, pinfo = with_env("SM_SELL_CB", "0", lambda: _sell(sm, rp, ci, va, n_cols, 0))
+    assert pinfo["sell_codebook"] == 0 and info["device_bytes"] < pinfo["device_bytes"]
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    x[0] = np.inf                       # what padding words point at
+    x[7::5003] = np.nan
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    y0[:40] = -0.0
+    for alpha, beta in ((1.0, 1.0), (1.7, 0.0), (-0.5, 2.0)):
+        ys = []
+        for A in (M, P):
+            y = to_dev(y0)
+            A.spmv(to_dev(x), y, alpha, beta)
+            ys.append(to_host(y))
+        assert np.array_equal(bits(ys[0]), bits(ys[1])), (alpha, beta)
+        lens = np.diff(np.asarray(rp, np.int64))
+        want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+        assert np.array_equal(bits(ys[0][lens <= 2048]), bits(want[lens <= 2048]))
 
 
 @pytest.mark.parametrize("sigma,streams", [(4096, 8), (4096, 1), (1000, 3)])
@@ -123,7 +161,7 @@ def test_sell_rmat_auto(sm):
     n = 1 << 20
     M = with_env("SM_XBAND", "0", lambda: sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n))
     info = M.info()
-    assert info["sell_slices"] > 0 and info["col_relabel"] == 1, info
+    assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
     rp, ci, va = rp_d.cpu().numpy(), ci_d.cpu().numpy(), va_d.cpu().numpy()
     rng = np.random.default_rng(9)
     x = rng.uniform(-1, 1, n).astype(np.float32)
