@@ -139,16 +139,20 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         const char *e = getenv("SM_SELL_UNROLL");
         return e ? atoi(e) : 8;
     }();
+#define SM_CSELL_K(U)                                                                          \
+    hipLaunchKernelGGL((spmv_csell_kernel<U>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,      \
+                       sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,                     \
+                       reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size,    \
+                       x, y, sd.d_partials, alpha, beta)
     if (sd.d_table) {
-        hipLaunchKernelGGL((spmv_csell_kernel<8>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
-                           sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
-                           reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size,
-                           x, y, sd.d_partials, alpha, beta);
+        if (unroll == 16) SM_CSELL_K(16);
+        else SM_CSELL_K(8);
     } else if (abl == 1) SM_SELL_K(8, 1);
     else if (unroll == 16) SM_SELL_K(16, 0);
     else if (unroll == 32) SM_SELL_K(32, 0);
     else SM_SELL_K(8, 0);
 #undef SM_SELL_K
+#undef SM_CSELL_K
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // Long rows: beta * y + their segment partials, in segment order.

@@ -5,19 +5,20 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_sell.py -x -q --timeout 120 --timeout-method thread \
+[ -n "$NO_TESTS" ] || timeout -k 10 300 python -u -m pytest tests/test_gpu_sell.py -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/csell_tests.log 2>&1 || { tail -30 gpurun_out/csell_tests.log; exit 1; }
-tail -2 gpurun_out/csell_tests.log
-for cb in 1 0; do
+[ -n "$NO_TESTS" ] || tail -2 gpurun_out/csell_tests.log
+for v in ${VARIANTS:-1:8 0:8}; do
+  cb=${v%%:*}; un=${v#*:}
   for wl in rmat uniform; do
     if [ $wl = rmat ]; then a="--workload rmat --scale 24 --tiles 2048 --replicas 1 --reps 5"
     else a="--workload uniform --rows 1048576 --tiles 4096 --replicas 4 --reps 10"; fi
-    d=gpurun_out/csell_${wl}_$cb
+    d=$GRAFT_REPO_ROOT/gpurun_out/csell_${wl}_${cb}_$un
     rm -rf $d
-    ( cd /tmp && SM_SELL=1 SM_XBAND=0 SM_SELL_CB=$cb timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    ( cd /tmp && SM_SELL=1 SM_XBAND=0 SM_SELL_CB=$cb SM_SELL_UNROLL=$un timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $d -o run -- python3 $GRAFT_REPO_ROOT/tools/spmv_sweep.py $a --algos sell --rounds 1 ) \
-        > $d.log 2>&1 || { echo "$wl cb=$cb failed"; tail -20 $d.log; exit 1; }
-    python3 - $d "$wl cb=$cb" <<'PY'
+        > $d.log 2>&1 || { echo "$wl $v failed"; tail -20 $d.log; exit 1; }
+    python3 - $d "$wl cb=$cb u=$un" <<'PY'
 import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
