@@ -24,11 +24,15 @@
  * (ascending column) order, exactly as the reference does, so results are
  * bit-identical to the reference CPU kernel.  SM_ALGO_XBAND keeps that order for
  * every row on the exact band layout (sm_info.has_xband == 1, or any layout with
- * xband_slabs == 1); the blocked layout (has_xband == 2) sums each column slab in
- * order and adds the slab sums in slab order.  SM_ALGO_STREAM and the SpMM
- * kernels keep the order for rows of up to SM_SERIAL_ROW_MAX terms and use a
- * tree sum for longer rows.  The bound for every non-exact case is
- * |y - y_ref| <= 1e-6 * sum|terms|.
+ * xband_slabs == 1); the slab layouts (has_xband 2-5) sum each column slab in
+ * order and add the slab sums in slab order.  SM_ALGO_SELL keeps it for every row
+ * of up to 2048 terms and adds longer rows' 2048-term segment sums in order.  The
+ * SpMM kernels keep it for every row.  SM_ALGO_STREAM keeps it for rows of up to
+ * SM_SERIAL_ROW_MAX terms and uses a tree sum for longer rows.  The bound for
+ * every non-exact case is |y - y_ref| <= 1e-6 * sum|terms|.
+ *
+ * Concurrency: calls on one matrix from several streams or threads are correct;
+ * SpMVs that use the matrix's scratch take turns on the device.
  *
  * Errors: every call returns sm_status; sm_last_error() gives a message for
  * the calling thread.  Device calls are asynchronous on `stream` (a
@@ -150,17 +154,69 @@ SM_API sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz,
                                     const float *val, int32_t device, sm_matrix **out);
 
 /* Same, from device pointers on `device` (copied device-to-device on `stream`
- * and validated by a kernel; synchronises `stream`). */
+ * and validated by a kernel; synchronises `stream`).  The layout builders run on
+ * the host: the columns (and, for the layout that stores them, the values) are
+ * copied to the host once, at creation -- 4 + 4 bytes per term over PCIe. */
 SM_API sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
                                            const int32_t *d_row_ptr, const int32_t *d_col_idx,
                                            const float *d_val, int32_t device, sm_stream stream,
                                            sm_matrix **out);
 
+/* ---- layout options ---------------------------------------------------------
+ * The constructors pick the SpMV layout themselves (SM_LAYOUT_AUTO).
+ * sm_create_from_csr_ex / _device_ex take these options instead, to force a layout
+ * (tests, A/B measurements).  Every layout computes the same product; they differ
+ * in speed and in where the bit-exact reference order holds (sm_info.has_xband).
+ * Fields past `struct_size` keep their defaults, so callers built against an
+ * older header stay valid.  Initialise with sm_build_opts_init. */
+typedef enum sm_layout {
+    SM_LAYOUT_AUTO = 0,      /* cost model: balanced codebook bands / bands / sell / stream */
+    SM_LAYOUT_EXACT = 1,     /* column bands, one slab: every row in the reference's order */
+    SM_LAYOUT_BLOCKED = 2,   /* column bands in slabs (x staged through LDS)               */
+    SM_LAYOUT_GATHER = 3,    /* column-ordered bands, x gathered                           */
+    SM_LAYOUT_BAND2 = 4,     /* balanced bands, 8-byte entries                             */
+    SM_LAYOUT_CBAND = 5,     /* balanced bands, 4-byte codebook words                      */
+    SM_LAYOUT_NO_BANDS = 6,  /* no band layout: sorted sliced-ELL, else the stream kernel   */
+    SM_LAYOUT_BANDS = 7      /* a band layout even where the cost model would decline; the
+                                kind as AUTO would pick it                                */
+} sm_layout;
+
+typedef struct sm_build_opts {
+    int32_t struct_size;       /* sizeof(sm_build_opts) as the caller compiled it      */
+    int32_t layout;            /* sm_layout                                            */
+    int32_t band_slabs;        /* balanced bands: column slabs per row block, 0 = auto  */
+    int32_t band_tall;         /* balanced bands: 1 = tall tiles (32K rows)            */
+    int32_t gather_band_log2;  /* gather bands: 13, 14 or 15 (log2 columns), 0 = auto  */
+    int32_t sell;              /* sorted sliced-ELL: -1 auto (built when no band layout), 0 never */
+    int32_t sell_codebook;     /* sell slots as column|id words: -1 auto, 0 never      */
+    int32_t sell_max_len;      /* rows longer than this are cut in segments, 0 = 2048  */
+    int32_t sell_streams;      /* XCD streams of sort windows, 0 = auto                */
+    int64_t sell_sigma;        /* sort rows by length within windows of this many rows, 0 = globally */
+    int32_t relabel;           /* column relabeling by degree: -1 auto, 0 never, 1 always */
+    int32_t tile_nnz;          /* stream-kernel tile: 1024/2048/4096/8192, 0 = auto   */
+} sm_build_opts;
+
+SM_API void sm_build_opts_init(sm_build_opts *opts);
+
+SM_API sm_status sm_create_from_csr_ex(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                       const int32_t *row_ptr, const int32_t *col_idx,
+                                       const float *val, int32_t device,
+                                       const sm_build_opts *opts, sm_matrix **out);
+SM_API sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                              const int32_t *d_row_ptr, const int32_t *d_col_idx,
+                                              const float *d_val, int32_t device,
+                                              sm_stream stream, const sm_build_opts *opts,
+                                              sm_matrix **out);
+
 /* Destroy: sparse-matrix.cc:9-18 (frees host and device storage). */
 SM_API void sm_destroy(sm_matrix *m);
 
 /* ---- queries ----------------------------------------------------------- */
+/* sm_info grew in 0.2 (xband_slab_cols, sell_slices, sell_codebook): a caller built
+ * against an older header passes its own sizeof to sm_get_info_ex, which writes only
+ * that many bytes.  sm_get_info writes the whole struct of this header. */
 SM_API sm_status sm_get_info(const sm_matrix *m, sm_info *info);
+SM_API sm_status sm_get_info_ex(const sm_matrix *m, sm_info *info, size_t info_bytes);
 SM_API int32_t sm_num_rows(const sm_matrix *m);   /* NumRows, sparse-matrix.h:39 */
 SM_API int32_t sm_num_cols(const sm_matrix *m);   /* NumCols, sparse-matrix.h:40 */
 
@@ -194,8 +250,11 @@ SM_API sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const f
 
 /* AddMatMat (sparse-matrix.cc:139-194) on device pointers:
  * C (m x n, ldc) = alpha * A (m x k, lda) * S + beta * C.
- * 2 <= m <= 128 with algo != SM_ALGO_PARITY: transposes + row-panel SpMM in a
- * per-call workspace; the call synchronises `stream` before returning. */
+ * m = 1: sm_spmv.  2 <= m <= 128 with algo != SM_ALGO_PARITY: transposes + row-panel
+ * SpMM in the matrix's workspace, asynchronous on `stream`: the stream first waits on
+ * an event recorded after the previous call's last use of the workspace (calls from
+ * any streams take turns on the device; the host blocks only when a larger m makes
+ * the workspace grow).  Otherwise one thread per output reads A and C in place. */
 SM_API sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
                               float *c, int32_t ldc, float alpha, float beta, sm_algo algo,
                               sm_stream stream);
@@ -225,6 +284,58 @@ SM_API sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t 
 
 /* Synchronise the stream and report asynchronous kernel errors. */
 SM_API sm_status sm_stream_sync(sm_stream stream);
+
+/* ---- multi-GPU: row partition + one RCCL all-gather per product ------------
+ * SURVEY.md §8(e).  One process per GPU of one node.  Rank r holds its rows of B
+ * (any contiguous split; sm_multi_partition gives the equal one) as an sm_matrix with
+ * GLOBAL column indices, so its n_cols is the global column count.  x is split in
+ * nranks equal slices (n_cols % nranks == 0): rank r supplies x[r*L, (r+1)*L),
+ * L = n_cols / nranks.  Per product the only exchange is one ncclAllGather of the x
+ * slices (SpMM: of the X panel's row slices) over xGMI into the context's buffer,
+ * then the local SpMV / SpMM on the same stream.  No other collective: the reference's
+ * panels already write disjoint outputs (sparse-matrix.cc:164-190).
+ * RCCL is loaded at run time (the copy already in the process if any); without it
+ * sm_multi_* return SM_ERR_NOT_SUPPORTED.  Errors: sm_multi_last_error(). */
+#define SM_UNIQUE_ID_BYTES 128
+typedef struct sm_unique_id { char internal[SM_UNIQUE_ID_BYTES]; } sm_unique_id;
+typedef struct sm_multi sm_multi;
+
+SM_API const char *sm_multi_last_error(void);
+/* Rows [r0, r1) of rank `rank` in the equal split of n rows (the first n % nranks ranks
+ * get one row more).  Pure arithmetic, no device. */
+SM_API sm_status sm_multi_partition(int64_t n, int32_t nranks, int32_t rank, int64_t *r0,
+                                    int64_t *r1);
+/* Rank 0 creates the id and passes it to every rank out of band (MPI, a file,
+ * torch.distributed). */
+SM_API sm_status sm_multi_unique_id(sm_unique_id *id);
+/* Collective: every rank calls it with the same id and nranks.  The context refers to
+ * `local` (not owned; keep it alive) and joins the communicator on its device. */
+SM_API sm_status sm_multi_create(const sm_unique_id *id, int32_t nranks, int32_t rank,
+                                 const sm_matrix *local, sm_multi **out);
+SM_API void sm_multi_destroy(sm_multi *mc);
+/* y_local = alpha * B_local * x + beta * y_local, x = all-gather of the x_local slices. */
+SM_API sm_status sm_multi_spmv(sm_multi *mc, float alpha, const float *x_local, float beta,
+                               float *y_local, sm_algo algo, sm_stream stream);
+/* Y_local (rows x n_rhs, ldy) = alpha * B_local * X + beta * Y_local; X_local is this
+ * rank's L x n_rhs row-major slice of X (contiguous, ldx = n_rhs). */
+SM_API sm_status sm_multi_spmm(sm_multi *mc, int32_t n_rhs, float alpha, const float *X_local,
+                               float beta, float *Y_local, int64_t ldy, sm_algo algo,
+                               sm_stream stream);
+/* `count` independent products x_local[i] -> y_local[i]: the all-gather of product i+1
+ * runs on the context's own stream beside the SpMV of product i on `stream` (two
+ * gather buffers alternate); still one all-gather per product.  Returns with all of
+ * the batch ordered before later work on `stream`. */
+SM_API sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, float alpha,
+                                     const float *const *x_local, float beta,
+                                     float *const *y_local, sm_algo algo, sm_stream stream);
+/* The all-gather alone (n_rhs = 1 for x), into the context's buffer; *x_full (optional)
+ * receives its device address, valid until the next call on the context. */
+SM_API sm_status sm_multi_allgather(sm_multi *mc, const float *x_local, int32_t n_rhs,
+                                    sm_stream stream, const float **x_full);
+/* Device timing of sm_multi_spmv / _spmm (HIP events around the all-gather and the
+ * local product); sm_multi_last_times waits for the last call and reports both. */
+SM_API sm_status sm_multi_set_timing(sm_multi *mc, int32_t on);
+SM_API sm_status sm_multi_last_times(sm_multi *mc, float *allgather_ms, float *compute_ms);
 
 #ifdef __cplusplus
 }

@@ -37,11 +37,21 @@ ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5
 EXPORTS = (
     "sm_version", "sm_status_string", "sm_last_error", "sm_device_count",
     "sm_create_from_dense_index", "sm_create_from_dense_index_device", "sm_create_from_csr",
-    "sm_create_from_csr_device",
-    "sm_destroy", "sm_get_info", "sm_num_rows", "sm_num_cols", "sm_copy_ref_stream",
+    "sm_create_from_csr_device", "sm_build_opts_init", "sm_create_from_csr_ex",
+    "sm_create_from_csr_device_ex",
+    "sm_destroy", "sm_get_info", "sm_get_info_ex", "sm_num_rows", "sm_num_cols", "sm_copy_ref_stream",
     "sm_copy_csr", "sm_to_dense", "sm_equal", "sm_spmv", "sm_spmm", "sm_addmatmat",
     "sm_addmatmat_host", "sm_beta_scale", "sm_transpose", "sm_panel_kernel", "sm_stream_sync",
+    "sm_multi_last_error", "sm_multi_partition", "sm_multi_unique_id", "sm_multi_create",
+    "sm_multi_destroy", "sm_multi_spmv", "sm_multi_spmm", "sm_multi_spmv_batch",
+    "sm_multi_allgather", "sm_multi_set_timing", "sm_multi_last_times",
 )
+
+SM_UNIQUE_ID_BYTES = 128
+
+
+class SmUniqueId(C.Structure):
+    _fields_ = [("internal", C.c_char * SM_UNIQUE_ID_BYTES)]
 
 
 class SmInfo(C.Structure):
@@ -55,6 +65,33 @@ class SmInfo(C.Structure):
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
         ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("reserved0", C.c_int32),
     ]
+
+
+# sm_layout
+LAYOUTS = {"auto": 0, "exact": 1, "blocked": 2, "gather": 3, "band2": 4, "cband": 5,
+           "no_bands": 6, "bands": 7}
+
+
+class SmBuildOpts(C.Structure):
+    _fields_ = [
+        ("struct_size", C.c_int32), ("layout", C.c_int32), ("band_slabs", C.c_int32),
+        ("band_tall", C.c_int32), ("gather_band_log2", C.c_int32), ("sell", C.c_int32),
+        ("sell_codebook", C.c_int32), ("sell_max_len", C.c_int32), ("sell_streams", C.c_int32),
+        ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
+    ]
+
+
+def build_opts(**kw) -> SmBuildOpts:
+    """sm_build_opts from keyword arguments (layout may be a name from LAYOUTS)."""
+    o = SmBuildOpts()
+    load().sm_build_opts_init(C.byref(o))
+    for k, v in kw.items():
+        if k == "layout" and isinstance(v, str):
+            v = LAYOUTS[v]
+        if k not in dict(SmBuildOpts._fields_):
+            raise TypeError(f"unknown build option {k!r}")
+        setattr(o, k, int(v))
+    return o
 
 
 class SparseMatrixError(RuntimeError):
@@ -82,8 +119,14 @@ def _declare(L):
         "sm_create_from_csr": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, C.POINTER(_vp)], C.c_int),
         "sm_create_from_csr_device": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp,
                                        C.POINTER(_vp)], C.c_int),
+        "sm_build_opts_init": ([C.POINTER(SmBuildOpts)], None),
+        "sm_create_from_csr_ex": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, C.POINTER(SmBuildOpts),
+                                   C.POINTER(_vp)], C.c_int),
+        "sm_create_from_csr_device_ex": ([_i64, _i64, _i64, _vp, _vp, _vp, _i32, _vp,
+                                          C.POINTER(SmBuildOpts), C.POINTER(_vp)], C.c_int),
         "sm_destroy": ([_vp], None),
         "sm_get_info": ([_vp, C.POINTER(SmInfo)], C.c_int),
+        "sm_get_info_ex": ([_vp, C.POINTER(SmInfo), C.c_size_t], C.c_int),
         "sm_num_rows": ([_vp], _i32),
         "sm_num_cols": ([_vp], _i32),
         "sm_copy_ref_stream": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
@@ -99,6 +142,18 @@ def _declare(L):
         "sm_panel_kernel": ([_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp, _i32,
                              _vp, _i32, _vp], C.c_int),
         "sm_stream_sync": ([_vp], C.c_int),
+        "sm_multi_last_error": ([], C.c_char_p),
+        "sm_multi_partition": ([_i64, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
+        "sm_multi_unique_id": ([C.POINTER(SmUniqueId)], C.c_int),
+        "sm_multi_create": ([C.POINTER(SmUniqueId), _i32, _i32, _vp, C.POINTER(_vp)], C.c_int),
+        "sm_multi_destroy": ([_vp], None),
+        "sm_multi_spmv": ([_vp, _f32, _vp, _f32, _vp, C.c_int, _vp], C.c_int),
+        "sm_multi_spmm": ([_vp, _i32, _f32, _vp, _f32, _vp, _i64, C.c_int, _vp], C.c_int),
+        "sm_multi_spmv_batch": ([_vp, _i32, _f32, C.POINTER(_vp), _f32, C.POINTER(_vp), C.c_int,
+                                 _vp], C.c_int),
+        "sm_multi_allgather": ([_vp, _vp, _i32, _vp, C.POINTER(_vp)], C.c_int),
+        "sm_multi_set_timing": ([_vp, _i32], C.c_int),
+        "sm_multi_last_times": ([_vp, C.POINTER(_f32), C.POINTER(_f32)], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -131,6 +186,12 @@ def check(status: int, where: str) -> None:
     if status != SM_OK:
         L = load()
         raise SparseMatrixError(status, where, (L.sm_last_error() or b"").decode())
+
+
+def check_multi(status: int, where: str) -> None:
+    if status != SM_OK:
+        L = load()
+        raise SparseMatrixError(status, where, (L.sm_multi_last_error() or b"").decode())
 
 
 def device_count() -> int:

@@ -124,11 +124,20 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
             if (count(clo, mid) <= (int64_t)kB2Chunks * 64) lo = mid; else hi = mid - 1;
         }
         int64_t chi = lo;
+        // A single column whose terms in this block need more than kB2Chunks chunks (a
+        // hub or dense column: > 2048 terms, or rows too far apart for one chunk's row
+        // span) is split by rows over several one-column bands: a band takes the rows
+        // that fill its 32 chunks, the next band the same column from the next row on.
+        // Each row still has one term in that column, so every row's terms stay in
+        // ascending column order across the bands.
+        bool split = false;
         for (;;) {   // pack; shrink chi until the band fits
             segs.clear();
             bool retry = false;
             int chunks = 0, fill = cap;
             int32_t base = 0;
+            const bool single = chi == clo + 1;
+            split = false;
             for (int64_t r = 0; r < nr && !retry; r++) {
                 const int32_t s = cur[(size_t)r];
                 int32_t n = 0;
@@ -140,7 +149,10 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
                     break;
                 }
                 const Seg g{(int32_t)r, s, n};
-                if (opens(fill, base, g)) { chunks++; fill = 0; base = g.rl; }
+                if (opens(fill, base, g)) {
+                    if (single && chunks == kB2Chunks) { split = true; break; }   // rest: next band
+                    chunks++; fill = 0; base = g.rl;
+                }
                 fill += n;
                 segs.push_back(g);
             }
@@ -167,7 +179,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
         }
         for (int k = 0; k <= c; k++)
             emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al, geom);
-        clo = chi;
+        if (!split) clo = chi;   // split: the column's remaining rows go to the next band
     }
     for (int64_t r = 0; r < nr; r++)
         if (cur[(size_t)r] != end[(size_t)r]) out.ok = false;   // unsorted columns

@@ -102,6 +102,9 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.sell.d_partials);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
+    if (m->scratch_ready) (void)hipEventDestroy(m->scratch_ready);
+    m->scratch_ready = nullptr;
+    m->scratch_recorded = false;
     m->d_ws = nullptr;
     m->ws_bytes = 0;
     m->ws_ready = nullptr;
@@ -110,11 +113,8 @@ void free_device(sm_matrix *m) {
     m->plan = Plan();
 }
 
-// Build the stream plan from a host row_ptr and upload it.
-// Tile size: kTileNnz unless SM_TILE_NNZ (1024/2048/4096/8192) overrides it
-// (tuning knob, read at matrix creation).
 // SM_DEBUG_SYNC=1: synchronise after every launch and report the failing call
-// (fault attribution during development; never set in benchmarks).
+// (fault attribution; it changes no result, only the timing).
 bool debug_sync() {
     static const bool on = [] {
         const char *e = getenv("SM_DEBUG_SYNC");
@@ -130,39 +130,98 @@ hipError_t after_launch(hipError_t e, hipStream_t s, const char *what) {
     return e;
 }
 
-int32_t tile_nnz_setting() {
-    const char *e = getenv("SM_TILE_NNZ");
-    if (!e) return kTileNnz;
-    const int v = atoi(e);
+// Layout options: the caller's sm_build_opts with defaults for what it leaves out
+// (struct_size) and, in -DSM_DEV builds only, the SM_* development variables on top.
+BuildOpts resolve_opts(const sm_build_opts *o) {
+    BuildOpts r;
+    if (o) {
+        sm_build_opts d;
+        sm_build_opts_init(&d);
+        const size_t n = std::min<size_t>(sizeof(d), (size_t)std::max<int32_t>(o->struct_size, 0));
+        memcpy(&d, o, n);
+        r.layout = d.layout;
+        r.band_slabs = d.band_slabs;
+        r.band_tall = d.band_tall;
+        r.gather_band_log2 = d.gather_band_log2;
+        r.sell = d.sell;
+        r.sell_codebook = d.sell_codebook;
+        r.sell_max_len = d.sell_max_len;
+        r.sell_streams = d.sell_streams;
+        r.sell_sigma = d.sell_sigma;
+        r.relabel = d.relabel;
+        r.tile_nnz = d.tile_nnz;
+    }
+    if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
+    if (const char *e = dev_env("SM_XBAND_KIND")) {
+        static const char *names[] = {"", "exact", "blocked", "gather", "band2", "cband"};
+        for (int k = 1; k <= 5; ++k)
+            if (strcmp(e, names[k]) == 0) r.layout = k;
+    }
+    if (const char *e = dev_env("SM_BAND_TALL")) r.band_tall = atoi(e);
+    if (const char *e = dev_env("SM_BAND2_SLABS")) r.band_slabs = atoi(e);
+    if (const char *e = dev_env("SM_XBAND_GBAND")) r.gather_band_log2 = atoi(e);
+    if (const char *e = dev_env("SM_RELABEL")) r.relabel = atoi(e);
+    if (const char *e = dev_env("SM_SELL")) r.sell = atoi(e) ? -1 : 0;
+    if (const char *e = dev_env("SM_SELL_CB")) r.sell_codebook = atoi(e) ? -1 : 0;
+    if (const char *e = dev_env("SM_SELL_MAX")) r.sell_max_len = atoi(e);
+    if (const char *e = dev_env("SM_SELL_SIGMA")) r.sell_sigma = atoll(e);
+    if (const char *e = dev_env("SM_SELL_STREAMS")) r.sell_streams = atoi(e);
+    if (const char *e = dev_env("SM_TILE_NNZ")) r.tile_nnz = atoi(e);
+    return r;
+}
+
+sm_status check_opts(const sm_build_opts *o) {
+    if (!o) return SM_OK;
+    if (o->struct_size < (int32_t)(2 * sizeof(int32_t)))
+        return fail(SM_ERR_INVALID_ARG, "sm_build_opts.struct_size %d: call sm_build_opts_init",
+                    o->struct_size);
+    const BuildOpts r = resolve_opts(o);
+    if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_BANDS)
+        return fail(SM_ERR_INVALID_ARG, "unknown layout %d", r.layout);
+    if (r.band_slabs < 0 || r.band_slabs > 16) return fail(SM_ERR_INVALID_ARG, "band_slabs not in [0, 16]");
+    if (r.gather_band_log2 != 0 && (r.gather_band_log2 < 13 || r.gather_band_log2 > 15))
+        return fail(SM_ERR_INVALID_ARG, "gather_band_log2 must be 0 or 13..15");
+    if (r.tile_nnz != 0 && r.tile_nnz != 1024 && r.tile_nnz != 2048 && r.tile_nnz != 4096 &&
+        r.tile_nnz != 8192)
+        return fail(SM_ERR_INVALID_ARG, "tile_nnz must be 0, 1024, 2048, 4096 or 8192");
+    if (r.sell_max_len < 0 || r.sell_streams < 0 || r.sell_sigma < 0)
+        return fail(SM_ERR_INVALID_ARG, "negative sell option");
+    return SM_OK;
+}
+
+int32_t tile_nnz_setting(const sm_matrix *m) {
+    const int v = m->opts.tile_nnz;
     return (v == 1024 || v == 2048 || v == 4096 || v == 8192) ? v : kTileNnz;
 }
 
-// Column-band layout.  Which one: SM_XBAND=0 disables it,
-// SM_XBAND=1 forces it; otherwise it is built when sweeping x through every
-// tile's LDS costs less than the random gathers it replaces.  Cost model from
-// profiles/r01_microbench.txt: a tile streams x into LDS at ~85 GB/s per CU
+bool kind_forced(const sm_matrix *m) {
+    return m->opts.layout >= SM_LAYOUT_EXACT && m->opts.layout <= SM_LAYOUT_CBAND;
+}
+
+// Column-band layout.  SM_LAYOUT_NO_BANDS disables it,
+// SM_LAYOUT_BANDS (or a forced kind) builds it; otherwise it is built when sweeping x
+// through every tile's LDS costs less than the random gathers it replaces.  Cost model
+// from profiles/r01_microbench.txt: a tile streams x into LDS at ~85 GB/s per CU
 // (~22 TB/s chip-wide) while 4-byte gathers run at 75-200 G/s by the size of x,
 // so the sweep wins while its bytes stay under ~20x the matrix's 8 B per term.
-// SM_XBAND_KIND=exact picks the bit-exact single-slab layout instead.
-// SM_XBAND_KIND=blocked|gather|band2 forces a kind.  Otherwise: band2 (balanced
-// bands, kernels_band2.hip: config 2 41.1 us vs 41.7 blocked, bit-identical; it
-// falls back to blocked when its bands would be < 70 % filled), or gather for
-// wide matrices -- measured per rank of the bench's row partition (1M rows, 16 terms
-// per row), blocked vs gather with 16K- / 32K-column bands: 1M columns
-// 46 vs 59 / -, 2M 59 vs 60 / 66, 4M 85 vs 77 / 73, 8M 145 vs - / 93 us.  Past ~3M
-// columns each blocked tile sweeps more x through LDS than gathering its terms' x costs.
+// AUTO's kind: cband (balanced bands of codebook words, kernels_band2.hip; band2 when
+// the values take more than 255 bit patterns; it falls back to blocked when its bands
+// would be < 70 % filled), or gather for wide matrices -- measured per rank of the
+// bench's row partition (1M rows, 16 terms per row), blocked vs gather
+// with 16K- / 32K-column bands: 1M columns 46 vs 59 / -, 2M 59 vs 60 / 66, 4M 85 vs
+// 77 / 73, 8M 145 vs - / 93 us.  Past ~3M columns each blocked tile sweeps more x
+// through LDS than gathering its terms' x costs.
 constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 20);   // gather kind: > 3M columns
 
 XbKind xband_kind_setting(const sm_matrix *m) {
-    const char *e = getenv("SM_XBAND_KIND");
-    if (e && strcmp(e, "exact") == 0) return kXbExact;
-    if (e && strcmp(e, "gather") == 0) return kXbGather;
-    if (e && strcmp(e, "blocked") == 0) return kXbBlocked;
-    if (e && strcmp(e, "band2") == 0) return kXbBand2;
-    if (e && strcmp(e, "cband") == 0) return kXbCband;
-    // cband (balanced bands, codebook words) where the values form a codebook of
-    // <= 255 entries, else band2; either declines to the blocked kind when its bands
-    // would be mostly padding (upload_band2).
+    switch (m->opts.layout) {
+    case SM_LAYOUT_EXACT: return kXbExact;
+    case SM_LAYOUT_BLOCKED: return kXbBlocked;
+    case SM_LAYOUT_GATHER: return kXbGather;
+    case SM_LAYOUT_BAND2: return kXbBand2;
+    case SM_LAYOUT_CBAND: return kXbCband;
+    default: break;
+    }
     return m->n_cols > kGatherCols ? kXbGather : kXbCband;
 }
 
@@ -180,10 +239,10 @@ static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
 }
 
 bool want_xband(const sm_matrix *m) {
-    const char *e = getenv("SM_XBAND");
-    if (e && atoi(e) == 0) return false;
+    const int32_t L = m->opts.layout;
+    if (L == SM_LAYOUT_NO_BANDS) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
-    if (e && atoi(e) == 1) return true;
+    if (L != SM_LAYOUT_AUTO) return true;   // a forced kind, or SM_LAYOUT_BANDS
     return xband_cost_ok(m, xband_kind_setting(m));
 }
 
@@ -192,16 +251,14 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
-    // Geometry: SM_BAND_TALL=1 / 0 forces the tall / wide tiles (xband.h B2Geom).
-    const char *tall_env = getenv("SM_BAND_TALL");
-    const bool tall = tall_env && atoi(tall_env) == 1;
+    // Geometry: band_tall = 1 takes the tall tiles (xband.h B2Geom).
+    const bool tall = m->opts.band_tall == 1;
     const B2Geom geom = !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, m->n_rows);
     const int64_t nblk = (m->n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
         1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
-    if (const char *e = getenv("SM_BAND2_SLABS"))   // development / tests: force the slab count
-        want = std::max(1, std::min(16, atoi(e)));
+    if (m->opts.band_slabs > 0) want = std::max(1, std::min(16, m->opts.band_slabs));
     std::vector<float> table;
     std::vector<uint8_t> ids;
     const bool cb = kind == kXbCband && codebook_ids(val, m->nnz, table, ids);
@@ -212,10 +269,8 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     std::vector<uint8_t>().swap(ids);
     // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
     // dummies (wide or very sparse matrices), the padding would cost more HBM bytes
-    // than the layout saves -- decline unless forced (SM_XBAND_KIND=band2).
-    const char *kind_env = getenv("SM_XBAND_KIND");
-    const bool forced = kind_env && (strcmp(kind_env, "band2") == 0 || strcmp(kind_env, "cband") == 0);
-    if (!forced && bh.n_bands > 0 &&
+    // than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
+    if (!kind_forced(m) && bh.n_bands > 0 &&
         (double)bh.real_terms < 0.7 * (double)bh.n_bands * kB2Chunks * 64)
         return SM_OK;
     const int64_t band_words = cb ? 2048 : 4096;
@@ -262,9 +317,7 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
                        XbKind kind) {
     if (kind == kXbBand2 || kind == kXbCband) {
         const sm_status st = upload_band2(m, rp, col, val, kind);
-        const char *e = getenv("SM_XBAND_KIND");
-        if (st == SM_OK && m->plan.xb.n_blocks == 0 &&
-            !(e && (strcmp(e, "band2") == 0 || strcmp(e, "cband") == 0)))
+        if (st == SM_OK && m->plan.xb.n_blocks == 0 && !kind_forced(m))
             return upload_xband(m, rp, col, val, kXbBlocked);   // declined: blocked kind
         return st;
     }
@@ -272,12 +325,12 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     // columns -- fewer bands, hence fewer per-band barriers, for the same terms (8M
     // columns: 93 us with 32K bands vs 122 with 8K); the rank field shrinks to 3 bits,
     // ample at < 0.25 terms per row per band.  A forced gather kind on a narrower
-    // matrix (SM_XBAND_KIND=gather) keeps 8K-column bands.  SM_XBAND_GBAND=13|14|15
-    // forces the band width (16K: measured slower than the blocked kind at 2M).
-    const char *gb = getenv("SM_XBAND_GBAND");
-    const int gband_log2 = gb && atoi(gb) == 15 ? kXbGatherWideBandLog2
-                           : gb && atoi(gb) == 14 ? kXbGatherWideBandLog2 - 1
-                           : gb && atoi(gb) == 13 ? kXbGatherBandLog2
+    // matrix keeps 8K-column bands.  gather_band_log2 = 13|14|15 forces the band width
+    // (16K: measured slower than the blocked kind at 2M).
+    const int gb = m->opts.gather_band_log2;
+    const int gband_log2 = gb == 15 ? kXbGatherWideBandLog2
+                           : gb == 14 ? kXbGatherWideBandLog2 - 1
+                           : gb == 13 ? kXbGatherBandLog2
                            : m->n_cols > kGatherCols ? kXbGatherWideBandLog2
                                                      : kXbGatherBandLog2;
     const XbBits bits = kind == kXbExact    ? xb_bits(kXbExactBandLog2, kXbExactRowsLog2)
@@ -295,8 +348,8 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
         // segments may still fit the blocked layout (5 bits, 8K-column bands).
         // Only where the blocked kind's own sweep cost still pays (its row blocks
         // differ from the gather kind's); otherwise the stream kernel serves it.
-        if (kind == kXbGather && !getenv("SM_XBAND_KIND") &&
-            (xband_cost_ok(m, kXbBlocked) || getenv("SM_XBAND")))
+        if (kind == kXbGather && !kind_forced(m) &&
+            (xband_cost_ok(m, kXbBlocked) || m->opts.layout == SM_LAYOUT_BANDS))
             return upload_xband(m, rp, col, val, kXbBlocked);
         return SM_OK;   // layout not applicable: the stream kernel serves this matrix
     }
@@ -342,17 +395,16 @@ sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, cons
     return SM_OK;
 }
 
-// Column relabeling for the stream kernel.  SM_RELABEL=0 disables
-// it, SM_RELABEL=1 forces it; otherwise it is built when x is larger than an XCD's
+// Column relabeling for the stream kernel.  relabel = 0 disables
+// it, 1 forces it; otherwise it is built when x is larger than an XCD's
 // L2 (>= 2^20 columns), no band layout serves the matrix, there are at least as many
 // terms as columns (the per-SpMV permutation of x is then cheap next to the
 // product), and the column degrees are skewed: the busiest 1/16 of the columns hold
 // >= 40 % of the terms (power-law graphs: R-MAT scale 24 has 87 % there).
 bool want_relabel_size(const sm_matrix *m) {
-    const char *e = getenv("SM_RELABEL");
-    if (e && atoi(e) == 0) return false;
+    if (m->opts.relabel == 0) return false;
     if (m->nnz == 0 || m->n_cols == 0) return false;
-    if (e && atoi(e) == 1) return true;
+    if (m->opts.relabel == 1) return true;
     return m->n_cols >= (1 << 20) && m->nnz >= m->n_cols && m->plan.xb.n_blocks == 0;
 }
 
@@ -372,8 +424,7 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
         perm[(size_t)j] = (int32_t)c;
         rank[(size_t)c] = (int32_t)j;
     }
-    const char *env = getenv("SM_RELABEL");
-    if (!(env && atoi(env) == 1)) {
+    if (m->opts.relabel != 1) {
         int64_t hot = 0;
         for (int64_t j = 0; j < nc / 16; j++) hot += deg[(size_t)perm[(size_t)j]];
         if ((double)hot < 0.4 * (double)nnz) return SM_OK;   // not skewed: no gain
@@ -399,8 +450,7 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
 // R-MAT (1.91 vs 2.30 ms), and every row up to kSellMaxLen terms is summed in the
 // reference's order (the stream kernel: rows up to 64).
 bool want_sell(const sm_matrix *m) {
-    const char *e = getenv("SM_SELL");
-    if (e && atoi(e) == 0) return false;
+    if (m->opts.sell == 0) return false;
     return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0;
 }
 
@@ -414,21 +464,17 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
         c = rcol.data();
     }
     // Rows up to max_len terms go to the slices (one lane each, in stored order); the
-    // longer ones as max_len-term segments.  SM_SELL_MAX overrides the cap.
-    int32_t max_len = kSellMaxLen;
-    if (const char *e = getenv("SM_SELL_MAX")) max_len = std::max(1, atoi(e));
-    // SM_SELL_SIGMA: sort within windows of that many rows (0: one window),
-    // SM_SELL_STREAMS: XCD streams of windows (default 8 with windows).
-    int64_t sigma = 0;
-    if (const char *e = getenv("SM_SELL_SIGMA")) sigma = std::max<int64_t>(0, atoll(e));
-    int streams = sigma > 0 ? 8 : 1;
-    if (const char *e = getenv("SM_SELL_STREAMS")) streams = std::max(1, atoi(e));
-    // Codebook form (SM_SELL_CB=0 disables it): values of <= 255 distinct bit patterns
-    // and columns < 2^24 -- one 4-byte word per slot instead of column + value.
+    // longer ones as max_len-term segments.  sell_max_len overrides the cap.
+    const int32_t max_len = m->opts.sell_max_len > 0 ? m->opts.sell_max_len : kSellMaxLen;
+    // sell_sigma: sort within windows of that many rows (0: one window),
+    // sell_streams: XCD streams of windows (default 8 with windows).
+    const int64_t sigma = std::max<int64_t>(0, m->opts.sell_sigma);
+    const int streams = m->opts.sell_streams > 0 ? m->opts.sell_streams : sigma > 0 ? 8 : 1;
+    // Codebook form (sell_codebook = 0 disables it): values of <= 255 distinct bit
+    // patterns and columns < 2^24 -- one 4-byte word per slot instead of column + value.
     std::vector<float> table;
     std::vector<uint8_t> ids;
-    const char *ecb = getenv("SM_SELL_CB");
-    const bool cb = !(ecb && atoi(ecb) == 0) && m->n_cols <= ((int64_t)1 << kSellCbColBits) &&
+    const bool cb = m->opts.sell_codebook != 0 && m->n_cols <= ((int64_t)1 << kSellCbColBits) &&
                     codebook_ids(val, m->nnz, table, ids);
     if (!cb) std::vector<uint8_t>().swap(ids);
     SellHost sh;
@@ -479,11 +525,11 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
 
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
-    int32_t tile = tile_nnz_setting();
+    int32_t tile = tile_nnz_setting(m);
     // Power-law rows (longest row > 64x the mean, e.g. R-MAT): 2048-term tiles
     // balance the workgroups better -- R-MAT scale 24: 2.34 ms vs 2.43 ms at 4096
-    // (profiles/r01_rmat24_sweep.txt).  SM_TILE_NNZ overrides.
-    if (!getenv("SM_TILE_NNZ") && m->n_rows > 0) {
+    // (profiles/r01_rmat24_sweep.txt).  tile_nnz overrides.
+    if (m->opts.tile_nnz == 0 && m->n_rows > 0) {
         int64_t longest = 0;
         for (int64_t r = 0; r < m->n_rows; r++)
             longest = std::max<int64_t>(longest, (int64_t)rp_host[r + 1] - rp_host[r]);
@@ -562,9 +608,10 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     return st2;
 }
 
-std::unique_ptr<sm_matrix> new_matrix(int32_t device) {
+std::unique_ptr<sm_matrix> new_matrix(int32_t device, const sm_build_opts *opts = nullptr) {
     std::unique_ptr<sm_matrix> m(new sm_matrix());
     m->device = device;
+    m->opts = resolve_opts(opts);
     return m;
 }
 
@@ -572,7 +619,7 @@ std::unique_ptr<sm_matrix> new_matrix(int32_t device) {
 
 extern "C" {
 
-const char *sm_version(void) { return "sparsematrix_amd 0.1 (gfx950)"; }
+const char *sm_version(void) { return "sparsematrix_amd 0.2 (gfx950)"; }
 
 const char *sm_status_string(sm_status s) {
     switch (s) {
@@ -758,12 +805,30 @@ sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows
     return st;
 }
 
+void sm_build_opts_init(sm_build_opts *o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->struct_size = (int32_t)sizeof(*o);
+    o->layout = SM_LAYOUT_AUTO;
+    o->sell = -1;
+    o->sell_codebook = -1;
+    o->relabel = -1;
+}
+
 sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *row_ptr,
                              const int32_t *col_idx, const float *val, int32_t device,
                              sm_matrix **out) {
+    return sm_create_from_csr_ex(n_rows, n_cols, nnz, row_ptr, col_idx, val, device, nullptr, out);
+}
+
+sm_status sm_create_from_csr_ex(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                                int32_t device, const sm_build_opts *opts, sm_matrix **out) {
     if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
     *out = nullptr;
-    sm_status st = check_sizes(n_rows, n_cols, nnz);
+    sm_status st = check_opts(opts);
+    if (st != SM_OK) return st;
+    st = check_sizes(n_rows, n_cols, nnz);
     if (st != SM_OK) return st;
     if (!row_ptr || (nnz > 0 && (!col_idx || !val)))
         return fail(SM_ERR_INVALID_ARG, "null CSR array");
@@ -781,7 +846,7 @@ sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz, const 
     if (st != SM_OK) return st;
     DeviceGuard g(device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-    auto m = new_matrix(device);
+    auto m = new_matrix(device, opts);
     m->n_rows = n_rows;
     m->n_cols = n_cols;
     m->nnz = nnz;
@@ -800,9 +865,19 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
                                     const int32_t *d_row_ptr, const int32_t *d_col_idx,
                                     const float *d_val, int32_t device, sm_stream stream,
                                     sm_matrix **out) {
+    return sm_create_from_csr_device_ex(n_rows, n_cols, nnz, d_row_ptr, d_col_idx, d_val, device,
+                                        stream, nullptr, out);
+}
+
+sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                       const int32_t *d_row_ptr, const int32_t *d_col_idx,
+                                       const float *d_val, int32_t device, sm_stream stream,
+                                       const sm_build_opts *opts, sm_matrix **out) {
     if (!out) return fail(SM_ERR_INVALID_ARG, "out is null");
     *out = nullptr;
-    sm_status st = check_sizes(n_rows, n_cols, nnz);
+    sm_status st = check_opts(opts);
+    if (st != SM_OK) return st;
+    st = check_sizes(n_rows, n_cols, nnz);
     if (st != SM_OK) return st;
     if (!d_row_ptr || (nnz > 0 && (!d_col_idx || !d_val)))
         return fail(SM_ERR_INVALID_ARG, "null CSR array");
@@ -811,7 +886,7 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
     DeviceGuard g(device);
     if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;
-    auto m = new_matrix(device);
+    auto m = new_matrix(device, opts);
     m->n_rows = n_rows;
     m->n_cols = n_cols;
     m->nnz = nnz;
@@ -849,20 +924,26 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
     }
     st = upload_plan(m.get(), rp.data());
     const bool xband = want_xband(m.get());
-    const char *sell_env = getenv("SM_SELL");
-    const bool maybe_sell = !(sell_env && atoi(sell_env) == 0) && nnz > 0;
+    const bool maybe_sell = m->opts.sell != 0 && nnz > 0;
+    // The band / sell builders run on the host (band2.cpp, xband.cpp, sell.cpp): the
+    // columns come down for any of them, the values only for the layout that stores
+    // them (4 + 4 bytes per term over PCIe once, at creation).
     if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell)) {
         std::vector<int32_t> ch((size_t)nnz);
-        std::vector<float> vh((size_t)nnz);
+        std::vector<float> vh;
+        auto values = [&]() -> sm_status {
+            if (vh.size() == (size_t)nnz) return SM_OK;
+            vh.resize((size_t)nnz);
+            const hipError_t ev = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
+            return ev == hipSuccess ? SM_OK : hip_fail(ev, "copy CSR values for the layout builder");
+        };
         hipError_t e3 = hipSuccess;
-        if (nnz) {
-            e3 = hipMemcpy(ch.data(), m->d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost);
-            if (e3 == hipSuccess && (xband || maybe_sell))
-                e3 = hipMemcpy(vh.data(), m->d_val, (size_t)nnz * 4, hipMemcpyDeviceToHost);
-        }
-        st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR for band layout / relabeling");
+        if (nnz) e3 = hipMemcpy(ch.data(), m->d_col, (size_t)nnz * 4, hipMemcpyDeviceToHost);
+        st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR columns for the layout builder");
+        if (st == SM_OK && xband) st = values();
         if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting(m.get()));
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
+        if (st == SM_OK && want_sell(m.get())) st = values();
         if (st == SM_OK && want_sell(m.get())) st = upload_sell(m.get(), rp.data(), ch.data(), vh.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }
@@ -871,7 +952,14 @@ sm_status sm_create_from_csr_device(int64_t n_rows, int64_t n_cols, int64_t nnz,
 }
 
 sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
-    if (!m || !info) return fail(SM_ERR_INVALID_ARG, "null argument");
+    return sm_get_info_ex(m, info, sizeof(sm_info));
+}
+
+sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
+    if (!m || !out) return fail(SM_ERR_INVALID_ARG, "null argument");
+    sm_info full;
+    memset(&full, 0, sizeof(full));
+    sm_info *info = &full;
     info->s_rows = m->s_rows;
     info->s_cols = m->s_cols;
     info->n_rows = m->n_rows;
@@ -899,6 +987,8 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;
     info->sell_codebook = m->plan.sell.d_table != nullptr;
+    // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
+    memcpy(out, &full, std::min(info_bytes, sizeof(full)));
     return SM_OK;
 }
 
@@ -989,6 +1079,25 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (beta != 1.0f) e = launch_beta(y, 1, n, n, beta, s);
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv beta");
     }
+    if (algo < SM_ALGO_AUTO || algo > SM_ALGO_SELL) return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
+    // The matrix's SpMV scratch (sm_internal.h): SpMVs that use it run one after the
+    // other on the device, whatever stream or thread issues them.
+    const Plan &pl = m->plan;
+    const bool scratch = algo != SM_ALGO_PARITY && algo != SM_ALGO_VECTOR &&
+                         ((pl.xb.n_blocks > 0 && pl.xb.n_slabs > 1) || pl.n_relabel > 0 ||
+                          pl.sell.n_long > 0 || pl.n_long > 0);
+    std::unique_lock<std::mutex> lk(m->scratch_mu, std::defer_lock);
+    bool ordered = false;
+    if (scratch) {
+        lk.lock();
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+        ordered = cs == hipStreamCaptureStatusNone;
+        if (ordered && !m->scratch_ready)
+            e = hipEventCreateWithFlags(&m->scratch_ready, hipEventDisableTiming);
+        if (ordered && e == hipSuccess && m->scratch_recorded) e = hipStreamWaitEvent(s, m->scratch_ready, 0);
+        if (e != hipSuccess) return hip_fail(e, "sm_spmv scratch ordering");
+    }
     switch (algo) {
     case SM_ALGO_PARITY:
         e = launch_spmv_parity(n, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta, s);
@@ -1034,6 +1143,11 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     default:
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     }
+    if (ordered) {   // whatever was queued (also on a failed launch) uses the scratch
+        const hipError_t er = hipEventRecord(m->scratch_ready, s);
+        if (er == hipSuccess) m->scratch_recorded = true;
+        if (e == hipSuccess) e = er;
+    }
     e = after_launch(e, s, "sm_spmv");
     return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv launch");
 }
@@ -1058,7 +1172,7 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND) algo = SM_ALGO_AUTO;   // SpMV layouts
     if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
         e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X,
-                                 ldx, m->n_cols, Y, ldy, alpha, beta, s);
+                                 ldx, m->n_cols, Y, ldy, alpha, beta, algo != SM_ALGO_VECTOR, s);
     else if (algo >= SM_ALGO_AUTO && algo <= SM_ALGO_VECTOR)
         e = launch_spmm_generic(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, X, ldx, 1, Y, ldy, 1,
                                 alpha, beta, true, s);
@@ -1110,13 +1224,18 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
             else mat->d_ws = nullptr;
         }
         float *X = mat->d_ws, *Y = mat->d_ws + k * mp;
+        bool queued = false;   // any kernel on the workspace: the next user must wait for it
         if (e == hipSuccess) e = launch_transpose(a, m, (int32_t)k, lda, X, mp, s);
+        queued = queued || e == hipSuccess;
         if (e == hipSuccess) e = launch_transpose(c, m, (int32_t)n, ldc, Y, mp, s);
         if (e == hipSuccess)
             e = launch_spmm_rowpanel((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val,
-                                     (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, s);
+                                     (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, true, s);
         if (e == hipSuccess) e = launch_transpose(Y, (int32_t)n, m, mp, c, ldc, s);
-        if (e == hipSuccess) e = hipEventRecord(mat->ws_ready, s);
+        if (queued) {   // recorded on the error path too: kernels may be queued
+            const hipError_t er = hipEventRecord(mat->ws_ready, s);
+            if (e == hipSuccess) e = er;
+        }
         e = after_launch(e, s, "sm_addmatmat");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat (row panels)");
     }

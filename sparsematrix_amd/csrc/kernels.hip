@@ -529,26 +529,34 @@ hipError_t launch_spmv_stream(const Plan &p, const int32_t *rp, const int32_t *c
                               float beta, float *partials, hipStream_t s) {
     const int64_t grid = (int64_t)p.n_chunks + p.n_tiles;
     if (grid == 0) return hipSuccess;
+#ifdef SM_DEV
     static const int abl = [] {
-        const char *e = getenv("SM_STREAM_ABLATE");
+        const char *e = dev_env("SM_STREAM_ABLATE");
         return e ? atoi(e) : 0;
     }();
+#define SM_STREAM_ABL(TT)                                                                     \
+    if (abl == 1) {                                                                           \
+        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT, 1>), dim3((unsigned)grid), \
+                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
+                           col, val, x, y, alpha, beta, partials);                            \
+        break;                                                                                \
+    }
+#else
+#define SM_STREAM_ABL(TT)
+#endif
 #define SM_STREAM(TT)                                                                         \
     case TT:                                                                                  \
-        if (abl == 1)                                                                         \
-            hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT, 1>), dim3((unsigned)grid), \
-                               dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
-                               col, val, x, y, alpha, beta, partials);                        \
-        else                                                                                  \
-            hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)grid), \
-                               dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
-                               col, val, x, y, alpha, beta, partials);                        \
+        SM_STREAM_ABL(TT)                                                                     \
+        hipLaunchKernelGGL((spmv_stream_kernel<kStreamThreads, TT>), dim3((unsigned)grid),    \
+                           dim3(kStreamThreads), 0, s, p.d_tiles, p.d_chunks, p.n_chunks, rp, \
+                           col, val, x, y, alpha, beta, partials);                            \
         break;
     switch (p.tile_nnz) {
         SM_STREAM(1024) SM_STREAM(2048) SM_STREAM(4096) SM_STREAM(8192)
         default: return hipErrorInvalidValue;
     }
 #undef SM_STREAM
+#undef SM_STREAM_ABL
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.n_long == 0) return e;
     hipLaunchKernelGGL(spmv_long_finalize_kernel, dim3(blocks_for(p.n_long)), dim3(256), 0, s,
@@ -599,16 +607,15 @@ hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const
 hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
                                 const float *val, int32_t nnz, const float *X, int64_t ldx,
                                 int64_t x_rows, float *Y, int64_t ldy, float alpha, float beta,
-                                hipStream_t s) {
+                                bool allow_pipelined, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     int G = 1;
     while (4 * G < nrhs) G <<= 1;
     const unsigned grid = blocks_for((int64_t)n * G);
     // The gather-pipelined kernel while its X descriptor can span X (< 4 GiB) and a
-    // group's gathers fit the registers (G <= 16, i.e. N <= 64); SM_SPMM_OLD=1
-    // (development) keeps the one-group-at-a-time kernel for comparison.
-    const char *old_env = getenv("SM_SPMM_OLD");
-    const bool pipelined = !(old_env && atoi(old_env) != 0) && G <= 16 &&
+    // group's gathers fit the registers (G <= 16, i.e. N <= 64); allow_pipelined =
+    // false (sm_spmm with SM_ALGO_VECTOR) keeps the one-group-at-a-time kernel.
+    const bool pipelined = allow_pipelined && G <= 16 &&
                            (uint64_t)x_rows * (uint64_t)ldx * 4u < 0xFFFFFFF0ull;
 #define SM_PANEL(GG)                                                                         \
     case GG:                                                                                 \

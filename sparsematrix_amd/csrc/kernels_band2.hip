@@ -471,19 +471,22 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         (cb && (!xb.d_table || xb.table_size < 0 || xb.table_size > (int32_t)kCbDummyId)) ||
         (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
         return hipErrorInvalidValue;
-    static const int abl = [] {
-        const char *e = getenv("SM_BAND2_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
-    static const int prio = [] {
-        const char *e = getenv("SM_BAND2_PRIO");
-        return e ? atoi(e) : 2;
-    }();
     const dim3 grid((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), block(kB2Threads);
 #define SM_B2(A, P, C, T)                                                                      \
     hipLaunchKernelGGL((spmv_band2_kernel<A, P, C, T>), grid, block, 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,   \
                        xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+#ifdef SM_DEV
+    // Development builds: ablations (SM_BAND2_ABLATE, results wrong) and the wave
+    // priority (SM_BAND2_PRIO) of DESIGN.md §3.4b's measurements.
+    static const int abl = [] {
+        const char *e = dev_env("SM_BAND2_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    static const int prio = [] {
+        const char *e = dev_env("SM_BAND2_PRIO");
+        return e ? atoi(e) : 2;
+    }();
     if (tall) {
         if (abl == 8) {
             if (cb) SM_B2(8, 2, true, true); else SM_B2(8, 2, false, true);
@@ -527,6 +530,13 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     case 16: SM_B2(16, 2, false, false); break;
     default: return hipErrorInvalidValue;
     }
+#else
+    if (tall) {
+        if (cb) SM_B2(0, 2, true, true); else SM_B2(0, 2, false, true);
+    } else {
+        if (cb) SM_B2(0, 2, true, false); else SM_B2(0, 2, false, false);
+    }
+#endif
 #undef SM_B2
     return hipGetLastError();
 }

@@ -127,23 +127,26 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
     static_assert(kSellUnroll % 8 == 0, "slice lengths are multiples of the unroll");
     // Unrolls past kSellUnroll read slots past a slice's padded length: those lanes'
     // row lengths stop the adds, and the reads stay inside the arrays' zero tail.
-    static const int abl = [] {
-        const char *e = getenv("SM_SELL_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
 #define SM_SELL_K(U, A)                                                                        \
     hipLaunchKernelGGL((spmv_sell_kernel<U, A>), dim3((unsigned)grid), dim3(kSellThreads), 0, s, \
                        sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len, sd.d_col,       \
                        sd.d_val, x, y, sd.d_partials, alpha, beta)
-    static const int unroll = [] {
-        const char *e = getenv("SM_SELL_UNROLL");
-        return e ? atoi(e) : 8;
-    }();
 #define SM_CSELL_K(U)                                                                          \
     hipLaunchKernelGGL((spmv_csell_kernel<U>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,      \
                        sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,                     \
                        reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size,    \
                        x, y, sd.d_partials, alpha, beta)
+#ifdef SM_DEV
+    // Development builds: the gather ablation (SM_SELL_ABLATE=1, results wrong) and the
+    // unroll A/B (SM_SELL_UNROLL).
+    static const int abl = [] {
+        const char *e = dev_env("SM_SELL_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    static const int unroll = [] {
+        const char *e = dev_env("SM_SELL_UNROLL");
+        return e ? atoi(e) : 8;
+    }();
     if (sd.d_table) {
         if (unroll == 16) SM_CSELL_K(16);
         else SM_CSELL_K(8);
@@ -151,6 +154,10 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
     else if (unroll == 16) SM_SELL_K(16, 0);
     else if (unroll == 32) SM_SELL_K(32, 0);
     else SM_SELL_K(8, 0);
+#else
+    if (sd.d_table) SM_CSELL_K(8);
+    else SM_SELL_K(8, 0);
+#endif
 #undef SM_SELL_K
 #undef SM_CSELL_K
     const hipError_t e = hipGetLastError();

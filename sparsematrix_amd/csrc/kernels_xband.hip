@@ -41,14 +41,14 @@ namespace {
 // SM_XBAND_LOADERS=0/4/8: waves that only stage x (0: every wave stages and applies).  Both for A/B comparisons; read once.
 bool xband_dma_setting() {
     static const bool on = [] {
-        const char *e = getenv("SM_XBAND_DMA");
+        const char *e = dev_env("SM_XBAND_DMA");
         return !(e && atoi(e) == 0);
     }();
     return on;
 }
 int xband_loaders_setting() {   // SM_XBAND_LOADERS = 0 (default), 4 or 8 loader waves
     static const int n = [] {
-        const char *e = getenv("SM_XBAND_LOADERS");
+        const char *e = dev_env("SM_XBAND_LOADERS");
         const int v = e ? atoi(e) : 0;
         return v == 4 || v == 8 ? v : 0;
     }();
@@ -594,14 +594,17 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
                        n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
                        xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
                        alpha, beta)
+#ifdef SM_DEV
+    // Development builds: loader-wave roles, the register ring on the blocked kind
+    // (SM_XBAND_DMA=0) and the wave priority A/B (SM_XBAND_PRIO).
     if (dma) {
         if constexpr (XRr == 4) {
             if (loaders == 8)
                 SM_XBL(0, 8);
             else if (loaders == 4)
                 SM_XBL(0, 4);
-            else if (ABL == 0 && getenv("SM_XBAND_PRIO") && atoi(getenv("SM_XBAND_PRIO")) != 2) {
-                const int pr = atoi(getenv("SM_XBAND_PRIO"));
+            else if (ABL == 0 && dev_env("SM_XBAND_PRIO") && atoi(dev_env("SM_XBAND_PRIO")) != 2) {
+                const int pr = atoi(dev_env("SM_XBAND_PRIO"));
 #define SM_XBP(P)                                                                                 \
     hipLaunchKernelGGL((spmv_xband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, 0, ABL, true, 0, P>), \
                        dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
@@ -617,6 +620,12 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
     } else {
         SM_XBL(XRr, 0);
     }
+#else
+    (void)loaders;
+    (void)dma;
+    if constexpr (XRr == 4) SM_XBL(0, 0);   // x by LDS-DMA
+    else SM_XBL(XRr, 0);                     // exact kind: register ring
+#endif
 #undef SM_XBL
     return hipGetLastError();
 }
@@ -624,10 +633,15 @@ hipError_t launch_tiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, cons
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2>
 hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                        float *y, float alpha, float beta, hipStream_t s) {
-    const char *abl_env = getenv("SM_XBAND_ABLATE");   // development only
+#ifdef SM_DEV
+    const char *abl_env = dev_env("SM_XBAND_ABLATE");   // development only: results wrong
     const int abl = abl_env ? atoi(abl_env) : 0;
-    // Loader waves on the LDS-DMA path (SM_XBAND_LOADERS, default none; a count whose
-    // applying waves would need more than kXbMaxCap chunks per band is halved).
+#else
+    constexpr int abl = 0;
+#endif
+    // Loader waves on the LDS-DMA path (SM_XBAND_LOADERS, development builds, default
+    // none; a count whose applying waves would need more than kXbMaxCap chunks per band
+    // is halved).
     constexpr bool kDmaKind = (1 << BAND_LOG2) / (4 * THREADS) <= 2;
     int loaders = kDmaKind && (abl == 0 || abl == 32) && xband_dma_setting()
                       ? xband_loaders_setting() : 0;
@@ -639,6 +653,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
     if (loaders != 8 && loaders != 4) loaders = 0;
     const int64_t cap = cap_for(loaders);
 #define SM_XBT(C, A) launch_tiles<THREADS, BAND_LOG2, ROWS_LOG2, C, A>(xb, n_rows, n_cols, x, y, alpha, beta, loaders, s)
+#ifdef SM_DEV
     if (abl) {
         if (cap > 4) return hipErrorInvalidValue;
         switch (abl) {
@@ -661,6 +676,7 @@ hipError_t launch_kind(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const
         default: return hipErrorInvalidValue;
         }
     }
+#endif
     if (cap <= 1) return SM_XBT(1, 0);
     if (cap <= 2) return SM_XBT(2, 0);
     if (cap <= 3) return SM_XBT(3, 0);
@@ -905,14 +921,21 @@ __global__ __launch_bounds__(THREADS) void spmv_gband_kernel(
 template <int THREADS, int BAND_LOG2, int ROWS_LOG2, int CAP>
 hipError_t launch_gtiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                          float *y, float alpha, float beta, hipStream_t s) {
+#define SM_GBL(EA, GA)                                                                            \
+    hipLaunchKernelGGL((spmv_gband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, EA, GA>),           \
+                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
+                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
+                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
+                       alpha, beta)
+#ifdef SM_DEV
     static const int look = [] {
-        const char *e = getenv("SM_XBAND_GLOOK");
+        const char *e = dev_env("SM_XBAND_GLOOK");
         if (!e) return 52;
         const int ea = atoi(e), ga = strchr(e, ',') ? atoi(strchr(e, ',') + 1) : 0;
         return 10 * ea + ga;
     }();
     static const int abl = [] {
-        const char *e = getenv("SM_GBAND_ABLATE");
+        const char *e = dev_env("SM_GBAND_ABLATE");
         return e ? atoi(e) : 0;
     }();
     if (abl) {
@@ -930,12 +953,6 @@ hipError_t launch_gtiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, con
         default: return hipErrorInvalidValue;
         }
     }
-#define SM_GBL(EA, GA)                                                                            \
-    hipLaunchKernelGGL((spmv_gband_kernel<THREADS, BAND_LOG2, ROWS_LOG2, CAP, EA, GA>),           \
-                       dim3((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), dim3(THREADS), 0, s,  \
-                       n_rows, n_cols, xb.block_rows, xb.n_bands, xb.n_slabs, xb.slab_bands,     \
-                       xb.d_chunk_start, xb.d_word, xb.d_val, x, y, xb.d_partials, xb.d_tickets, \
-                       alpha, beta)
     switch (look) {
     case 32: SM_GBL(3, 2); break;
     case 62: SM_GBL(6, 2); break;
@@ -943,6 +960,9 @@ hipError_t launch_gtiles(const XbandDev &xb, int32_t n_rows, int32_t n_cols, con
     case 73: SM_GBL(7, 3); break;
     default: SM_GBL(5, 2); break;
     }
+#else
+    SM_GBL(5, 2);   // entries 5 bands ahead, x gathers 2
+#endif
 #undef SM_GBL
     return hipGetLastError();
 }

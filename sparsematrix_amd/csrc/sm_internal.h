@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -21,6 +22,34 @@ constexpr int kTileRows = 1024;           // row cap per tile (empty-row heavy g
 constexpr int kLongChunk = 4096;          // terms per workgroup for rows > kTileNnz
 constexpr int kSerialRowMax = SM_SERIAL_ROW_MAX;  // rows summed in reference order
 constexpr int kPadElems = 64;             // zero tail on col/val for aligned x4 loads
+
+// Development knobs.  Builds with -DSM_DEV (tools/*_ab.sh) read SM_* environment
+// variables for A/B measurements and ablations; the shipped library reads none of
+// them (a stray variable cannot change a caller's layouts or results) and holds no
+// ablation kernels.  Layout choices reach it only through sm_build_opts.
+inline const char *dev_env(const char *name) {
+#ifdef SM_DEV
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// Resolved layout options (sm_build_opts with defaults filled in).
+struct BuildOpts {
+    int32_t layout = SM_LAYOUT_AUTO;
+    int32_t band_slabs = 0;
+    int32_t band_tall = 0;
+    int32_t gather_band_log2 = 0;
+    int32_t sell = -1;
+    int32_t sell_codebook = -1;
+    int32_t sell_max_len = 0;
+    int32_t sell_streams = 0;
+    int64_t sell_sigma = 0;
+    int32_t relabel = -1;
+    int32_t tile_nnz = 0;
+};
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
 // holds a row longer than kSerialRowMax (wave-parallel reduction pass needed).
@@ -130,7 +159,7 @@ hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const
 hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
                                 const float *val, int32_t nnz, const float *X, int64_t ldx,
                                 int64_t x_rows, float *Y, int64_t ldy, float alpha, float beta,
-                                hipStream_t s);
+                                bool allow_pipelined, hipStream_t s);
 hipError_t launch_beta(float *c, int32_t m, int32_t n, int64_t ldc, float beta, hipStream_t s);
 hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, float *sa,
                             int64_t ldsa, hipStream_t s);
@@ -168,6 +197,7 @@ struct sm_matrix {
     int32_t *d_col = nullptr;
     float *d_val = nullptr;
     smamd::Plan plan;
+    smamd::BuildOpts opts;                     // layout options the matrix was built with
     int64_t device_bytes = 0;
     // Reference encoding (only for matrices built by sm_create_from_dense_index).
     bool has_ref = false;
@@ -184,4 +214,14 @@ struct sm_matrix {
     mutable float *d_ws = nullptr;
     mutable size_t ws_bytes = 0;
     mutable hipEvent_t ws_ready = nullptr;
+    // SpMV scratch (slab partials and hand-off words, long-row partials, the relabeled
+    // x) belongs to the matrix: every SpMV that uses it makes its stream wait on
+    // scratch_ready (recorded after the previous such SpMV's kernels), so SpMVs on one
+    // matrix from several streams or threads run one after the other on the device,
+    // correct, the way the reference's read-only AddMatMat allows concurrent callers
+    // (sparse-matrix.cc:139-194).  Calls into a stream being captured are ordered by
+    // that stream alone.
+    mutable std::mutex scratch_mu;
+    mutable hipEvent_t scratch_ready = nullptr;
+    mutable bool scratch_recorded = false;
 };

@@ -85,3 +85,111 @@ def allgather_spmv_pipelined(products, group=None):
         cur[0](cur[2], cur[3])
         n += 1
     return n
+
+
+def partition_c(n_rows: int, world: int, rank: int) -> tuple[int, int]:
+    """The C ABI's equal split (sm_multi_partition); RowPartition.bounds restates it."""
+    import ctypes as C
+    from . import _lib
+    r0, r1 = C.c_int64(), C.c_int64()
+    _lib.check_multi(_lib.load().sm_multi_partition(n_rows, world, rank, C.byref(r0), C.byref(r1)),
+                     "sm_multi_partition")
+    return int(r0.value), int(r1.value)
+
+
+class MultiContext:
+    """The C ABI's multi-GPU context (sm_multi_*, include/sparsematrix.h): one RCCL
+    communicator over the ranks, one ncclAllGather of x per product, then the local
+    SpMV.  `local` is this rank's rows of B with global columns (a SparseMatrix);
+    `unique_id` the 128 bytes rank 0 made with MultiContext.unique_id() and handed to
+    every rank (bench.py broadcasts it over torch.distributed's gloo group)."""
+
+    def __init__(self, local, nranks: int, rank: int, unique_id: bytes):
+        import ctypes as C
+        from . import _lib
+        self._L = _lib.load()
+        self.local = local                       # the context refers to it: keep it alive
+        uid = _lib.SmUniqueId()
+        C.memmove(C.addressof(uid), bytes(unique_id), _lib.SM_UNIQUE_ID_BYTES)
+        h = C.c_void_p()
+        _lib.check_multi(self._L.sm_multi_create(C.byref(uid), nranks, rank, local._require(),
+                                                 C.byref(h)), "sm_multi_create")
+        self._h = h
+        self.nranks, self.rank = nranks, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from . import _lib
+        uid = _lib.SmUniqueId()
+        _lib.check_multi(_lib.load().sm_multi_unique_id(C.byref(uid)), "sm_multi_unique_id")
+        return C.string_at(C.addressof(uid), _lib.SM_UNIQUE_ID_BYTES)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.sm_multi_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _stream(t, stream) -> int:
+        if stream is not None:
+            return int(stream) if isinstance(stream, int) else int(stream.cuda_stream)
+        import torch
+        return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def spmv(self, x_local, y_local, alpha=1.0, beta=1.0, algo="auto", stream=None):
+        from . import _lib
+        from .sparse_matrix import _algo
+        _lib.check_multi(self._L.sm_multi_spmv(self._h, alpha, x_local.data_ptr(), beta,
+                                               y_local.data_ptr(), _algo(algo),
+                                               self._stream(y_local, stream)), "sm_multi_spmv")
+        return y_local
+
+    def spmm(self, X_local, Y_local, alpha=1.0, beta=1.0, algo="auto", stream=None):
+        from . import _lib
+        from .sparse_matrix import _algo
+        n_rhs = int(Y_local.shape[1])
+        assert X_local.is_contiguous() and X_local.shape[1] == n_rhs
+        _lib.check_multi(self._L.sm_multi_spmm(self._h, n_rhs, alpha, X_local.data_ptr(), beta,
+                                               Y_local.data_ptr(), int(Y_local.stride(0)),
+                                               _algo(algo), self._stream(Y_local, stream)),
+                         "sm_multi_spmm")
+        return Y_local
+
+    def spmv_batch(self, xs, ys, alpha=1.0, beta=1.0, algo="auto", stream=None):
+        import ctypes as C
+        from . import _lib
+        from .sparse_matrix import _algo
+        n = len(xs)
+        xa = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
+        ya = (C.c_void_p * n)(*[y.data_ptr() for y in ys])
+        _lib.check_multi(self._L.sm_multi_spmv_batch(self._h, n, alpha, xa, beta, ya, _algo(algo),
+                                                     self._stream(ys[0], stream)),
+                         "sm_multi_spmv_batch")
+
+    def allgather(self, x_local, n_rhs: int = 1, stream=None) -> int:
+        import ctypes as C
+        from . import _lib
+        p = C.c_void_p()
+        _lib.check_multi(self._L.sm_multi_allgather(self._h, x_local.data_ptr(), n_rhs,
+                                                    self._stream(x_local, stream), C.byref(p)),
+                         "sm_multi_allgather")
+        return int(p.value or 0)
+
+    def set_timing(self, on: bool) -> None:
+        from . import _lib
+        _lib.check_multi(self._L.sm_multi_set_timing(self._h, 1 if on else 0), "sm_multi_set_timing")
+
+    def last_times(self) -> tuple[float, float]:
+        import ctypes as C
+        from . import _lib
+        a, b = C.c_float(), C.c_float()
+        _lib.check_multi(self._L.sm_multi_last_times(self._h, C.byref(a), C.byref(b)),
+                         "sm_multi_last_times")
+        return float(a.value), float(b.value)

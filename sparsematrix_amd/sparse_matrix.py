@@ -157,26 +157,30 @@ class SparseMatrix:
 
     @classmethod
     def from_csr(cls, row_ptr, col_idx, val, n_cols: int, device: int = 0,
-                 stream=None) -> "SparseMatrix":
-        """Additive CSR ingestion of B (n_rows x n_cols): numpy (host) or torch cuda tensors."""
+                 stream=None, opts: Optional[dict] = None) -> "SparseMatrix":
+        """Additive CSR ingestion of B (n_rows x n_cols): numpy (host) or torch cuda tensors.
+
+        `opts` (optional) forces the SpMV layout, e.g. ``{"layout": "exact"}`` or
+        ``{"layout": "cband", "band_slabs": 1}`` -- the fields of sm_build_opts."""
         self = cls(device=device)
         n_rows = int(row_ptr.shape[0]) - 1
         nnz = int(col_idx.shape[0])
         h = C.c_void_p()
+        o = _lib.build_opts(**(opts or {}))
         if _is_device(row_ptr):
             import torch
             assert row_ptr.dtype == torch.int32 and col_idx.dtype == torch.int32
             assert val.dtype == torch.float32
             rp, ci, va = row_ptr.contiguous(), col_idx.contiguous(), val.contiguous()
-            st = self._L.sm_create_from_csr_device(n_rows, n_cols, nnz, _ptr(rp), _ptr(ci),
-                                                   _ptr(va), device, _stream_of(rp, stream),
-                                                   C.byref(h))
+            st = self._L.sm_create_from_csr_device_ex(n_rows, n_cols, nnz, _ptr(rp), _ptr(ci),
+                                                      _ptr(va), device, _stream_of(rp, stream),
+                                                      C.byref(o), C.byref(h))
         else:
             rp = np.ascontiguousarray(row_ptr, np.int32)
             ci = np.ascontiguousarray(col_idx, np.int32)
             va = np.ascontiguousarray(val, np.float32)
-            st = self._L.sm_create_from_csr(n_rows, n_cols, nnz, _ptr(rp), _ptr(ci), _ptr(va),
-                                            device, C.byref(h))
+            st = self._L.sm_create_from_csr_ex(n_rows, n_cols, nnz, _ptr(rp), _ptr(ci), _ptr(va),
+                                               device, C.byref(o), C.byref(h))
         check(st, "from_csr")
         self._h = h
         return self
@@ -192,7 +196,7 @@ class SparseMatrix:
 
     def info(self) -> dict:
         inf = SmInfo()
-        check(self._L.sm_get_info(self._require(), C.byref(inf)), "sm_get_info")
+        check(self._L.sm_get_info_ex(self._require(), C.byref(inf), C.sizeof(inf)), "sm_get_info")
         return {k: getattr(inf, k) for k, _ in SmInfo._fields_}
 
     @property

@@ -11,7 +11,7 @@ import pytest
 
 import oracle
 from gpu_util import (assert_terms_close, bits, slab_order_spmv, to_dev, to_host, torch_dev,
-                      uniform_csr, with_env)
+                      uniform_csr)
 
 pytestmark = pytest.mark.gpu
 
@@ -36,11 +36,8 @@ def _codebook(va, n=200, seed=0):
 
 
 def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
-    def make():
-        return with_env("SM_XBAND_KIND", kind, lambda: with_env(
-            "SM_BAND_TALL", str(tall), lambda: with_env(
-                "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))))
-    M = with_env("SM_BAND2_SLABS", str(slabs), make) if slabs else make()
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols,
+                                 opts=dict(layout=kind, band_tall=tall, band_slabs=slabs or 0))
     info = M.info()
     assert info["has_xband"] == KINDS[kind], info
     assert info["xband_block_rows"] <= (32768 if tall else 16384), info
@@ -188,8 +185,8 @@ def test_band2_config2_equals_blocked(sm):
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
     Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n)
-    Mb2 = with_env("SM_XBAND_KIND", "band2", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n))
-    Mbl = with_env("SM_XBAND_KIND", "blocked", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n))
+    Mb2 = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="band2"))
+    Mbl = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="blocked"))
     ic, i2, ib = Mcb.info(), Mb2.info(), Mbl.info()
     assert ic["has_xband"] == 5 and i2["has_xband"] == 4 and ib["has_xband"] == 2
     assert ic["xband_slabs"] == i2["xband_slabs"] == ib["xband_slabs"] == 4
@@ -210,7 +207,7 @@ def test_cband_falls_back_without_codebook(sm):
     """More than 255 distinct values: AUTO builds band2 (8-byte entries) instead."""
     rp, ci, va = uniform_csr(50000, 60000, 8, seed=5)
     va = np.random.default_rng(6).uniform(-1, 1, va.size).astype(np.float32)
-    M = with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, 60000))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, 60000, opts=dict(layout="bands"))
     assert M.info()["has_xband"] == 4
 
 
@@ -222,8 +219,7 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     import sparsematrix_amd.synth as synth
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
-    M = with_env("SM_XBAND_KIND", kind, lambda: with_env(
-        "SM_BAND_TALL", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n)))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout=kind, band_tall=1))
     info = M.info()
     assert info["has_xband"] == KINDS[kind] and info["xband_block_rows"] == 32768, info
     assert info["xband_slabs"] == 8 and info["xband_slab_cols"] == 131072, info
@@ -236,3 +232,95 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
                            to_host(y0), 1.3, 0.5, 131072)
     assert np.array_equal(bits(to_host(y)), bits(want))
+
+
+def test_config2_auto_full_size_vs_oracle(sm):
+    """BASELINE config 2 exactly as bench.py runs it (2^20 x 2^20, 16 distinct columns
+    per row, seed 2; AUTO = cband, 4 slabs of 262144 columns, alpha 1, beta 0.5):
+    bit-identical to the 4-slab restatement of the reference order on the oracle, and
+    within 1e-6 * sum|terms| of the reference's own per-row order (oracle.csr_spmv)."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    info = M.info()
+    assert info["has_xband"] == 5 and info["xband_slabs"] == 4, info
+    assert info["xband_slab_cols"] == 262144, info
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.0, 0.5)
+    got = to_host(y)
+    rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+    xh, y0h = to_host(x), to_host(y0)
+    want = slab_order_spmv(rph, cih, vah, xh, y0h, 1.0, 0.5, 262144)
+    assert np.array_equal(bits(got), bits(want))
+    ref = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.0, 0.5, threads=16)
+    _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.0, 0.5)
+    assert_terms_close(got, ref, absum)
+    # normwise too (SURVEY §8c: <= 1e-6 relative in the 2-norm)
+    assert np.linalg.norm(got.astype(np.float64) - ref) <= 1e-6 * np.linalg.norm(ref)
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+def test_band2_dense_columns_split_by_rows(sm, kind):
+    """Hub columns: every row holds column 4097 and every third row column 9000, so
+    one column of one 16K-row block needs more than a band's 32 chunks.  The builder
+    splits such a column by rows over one-column bands (it used to loop forever);
+    AUTO and the forced kinds stay bit-exact against the (slab-order) oracle."""
+    n_rows, n_cols = 40000, 20000
+    rng = np.random.default_rng(12)
+    rows = []
+    for r in range(n_rows):
+        c = {4097, *rng.integers(0, n_cols, 6).tolist()}
+        if r % 3 == 0:
+            c.add(9000)
+        rows.append(np.array(sorted(c), np.int32))
+    rp = np.zeros(n_rows + 1, np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    ci = np.concatenate(rows)
+    va = _codebook(rng.uniform(-1, 1, ci.size).astype(np.float32))
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    for slabs in (1, None):
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
+        _check(M, info, rp, ci, va, x, y0, 1.3, 0.7)
+    A = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)        # AUTO builds (and serves) it too
+    y = to_dev(y0)
+    A.spmv(to_dev(x), y, 1.3, 0.7)
+    ref = oracle.csr_spmv(rp, ci, va, x, y0, 1.3, 0.7)
+    _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, 1.3, 0.7)
+    assert_terms_close(to_host(y), ref, absum)
+
+
+def test_concurrent_spmvs_on_two_streams(sm):
+    """SpMVs on one matrix from two streams at once (the reference's AddMatMat only reads
+    the object, so concurrent callers are fine there, sparse-matrix.cc:139-194).  The
+    multi-slab layout's partial sums and hand-off words belong to the matrix; the library
+    orders such SpMVs on the device, so every result equals the one-stream result."""
+    torch = torch_dev()
+    n_rows, n_cols = 300000, 400000
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=31)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    info = M.info()
+    assert info["has_xband"] == 5 and info["xband_slabs"] > 1, info
+    rng = np.random.default_rng(32)
+    xs = [to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32)) for _ in range(8)]
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    want = [slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"])
+            for x in xs]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ys = [to_dev(y0) for _ in xs]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            y.copy_(torch.from_numpy(y0).cuda())
+        torch.cuda.synchronize()
+        for i, (x, y) in enumerate(zip(xs, ys)):
+            with torch.cuda.stream(streams[i % 2]):
+                M.spmv(x, y, 1.0, 0.5)
+        torch.cuda.synchronize()
+        for i, y in enumerate(ys):
+            assert np.array_equal(bits(to_host(y)), bits(want[i])), (rep, i)

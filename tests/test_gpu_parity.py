@@ -206,7 +206,7 @@ def test_spmm_n32_vs_oracle(sm):
 def test_spmm_ragged_all_panel_widths(sm, old):
     """Row panels of every width (N = 4 .. 128, G = 1 .. 32 lanes per row) on ragged
     rows (empty, shorter and longer than one 16-term group), with signed zeros;
-    SM_SPMM_OLD=1 runs the one-group-at-a-time kernel, 0 the gather-pipelined one
+    algo "vector" runs the one-group-at-a-time kernel, "auto" the gather-pipelined one
     (kernels.hip).  Bit-exact against the oracle."""
     n_rows, n_cols = 3000, 5000
     rng = np.random.default_rng(21)
@@ -226,7 +226,7 @@ def test_spmm_ragged_all_panel_widths(sm, old):
         for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (-2.0, 0.0)):
             want = oracle.csr_spmm(rp.astype(np.int64), ci, va, X, Y0, alpha, beta)
             Y = to_dev(Y0)
-            _with_env("SM_SPMM_OLD", old, lambda: M.spmm(to_dev(X), Y, alpha, beta))
+            M.spmm(to_dev(X), Y, alpha, beta, algo="vector" if old == "1" else "auto")
             assert bits_equal(to_host(Y), want), (N, alpha, beta)
 
 
@@ -414,27 +414,13 @@ def test_panel_kernels_vs_golden(sm):
 
 
 # ---------------------------------------------------------------------------- column-band kernel
-def _with_env(key, value, fn):
-    import os
-    old = os.environ.get(key)
-    os.environ[key] = value
-    try:
-        return fn()
-    finally:
-        if old is None:
-            os.environ.pop(key, None)
-        else:
-            os.environ[key] = old
-
-
 @pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 300001, 16), (9000, 70001, 40),
                                                    (4096, 32768, 7), (5000, 1000, 5)])
 def test_xband_bit_exact_vs_oracle(sm, n_rows, n_cols, per_row):
     """LDS-staged column-band SpMV: every row in reference order (bit-exact), incl.
     partial last band/block, n_cols not a multiple of 4, dense bands (rank rounds)."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols)
-    M = _with_env("SM_XBAND_KIND", "exact", lambda: _with_env(
-        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout="exact"))
     info = M.info()
     assert info["has_xband"] == 1 and info["xband_slabs"] == 1, info
     rng = np.random.default_rng(1)
@@ -456,8 +442,7 @@ def test_xband_blocked_vs_oracle(sm, n_rows, n_cols, per_row, kind, code):
     of the reference order; bit-identical when the matrix is a single slab; the
     AUTO path runs it; beta = 0 drops NaN only where the reference does."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols + 7)
-    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
-        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout=kind))
     info = M.info()
     assert info["has_xband"] == code, info
     assert info["xband_block_rows"] >= 64 and info["xband_slabs"] >= 1
@@ -486,8 +471,7 @@ def test_xband_special_values(sm, kind):
     va = va.copy()
     va[::997] = np.inf
     va[5::1009] = np.nan
-    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
-        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout=kind))
     assert M.info()["has_xband"] == {"exact": 1, "blocked": 2, "gather": 3}[kind]
     rng = np.random.default_rng(8)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
@@ -519,8 +503,7 @@ def test_xband_blocked_signed_zeros(sm, kind, code):
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=79)
     va = va.copy()
     va[6 * 100:6 * 200] = -0.0
-    M = _with_env("SM_XBAND_KIND", kind, lambda: _with_env(
-        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout=kind))
     assert M.info()["has_xband"] == code and M.info()["xband_slabs"] > 1, M.info()
     rng = np.random.default_rng(10)
     x = rng.uniform(0.25, 1, n_cols).astype(np.float32)
@@ -545,7 +528,7 @@ def test_xband_not_applicable_falls_back(sm):
     lengths = np.full(n_rows, 3)
     lengths[17] = 200            # 200 sorted columns in [0, 40000): ~41 per 8192-column band
     rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=2)
-    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout="bands"))
     assert M.info()["has_xband"] == 0
     rng = np.random.default_rng(3)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
@@ -557,7 +540,7 @@ def test_xband_not_applicable_falls_back(sm):
     assert_terms_close(to_host(y), want, ab)
     # unaligned x on a matrix that has the layout
     rp2, ci2, va2 = uniform_csr(5000, 40000, 8, seed=5)
-    M2 = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp2, ci2, va2, 40000))
+    M2 = sm.SparseMatrix.from_csr(rp2, ci2, va2, 40000, opts=dict(layout="bands"))
     assert M2.info()["has_xband"] == 2
     xb = torch.zeros(40001, dtype=torch.float32, device="cuda")
     xb[1:] = to_dev(x)
@@ -617,12 +600,8 @@ def test_relabel_bit_identical(sm, n_rows, n_cols, per_row, force):
     relabeling; terms keep their stored order, so the result is bit-identical to the
     unrelabeled stream kernel (and to the oracle on rows of <= 64 terms)."""
     rp, ci, va = _powerlaw_cols_csr(n_rows, n_cols, per_row, seed=n_cols)
-    env = "1" if force else None
-    if env:
-        M = _with_env("SM_RELABEL", env, lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
-    else:
-        M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
-    M0 = _with_env("SM_RELABEL", "0", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(relabel=1) if force else None)
+    M0 = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(relabel=0))
     assert M.info()["col_relabel"] == 1 and M0.info()["col_relabel"] == 0, M.info()
     rng = np.random.default_rng(2)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
@@ -689,8 +668,8 @@ def test_xband_gather_wide_bands_vs_oracle(sm, n_rows, n_cols, per_row, gband):
     3M columns): within the Σ|terms| bound, bit-identical when one slab; NaN in y dropped
     only by β = 0."""
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_cols + 11)
-    M = _with_env("SM_XBAND_GBAND", str(gband), lambda: _with_env("SM_XBAND_KIND", "gather", lambda: _with_env(
-        "SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols,
+                                 opts=dict(layout="gather", gather_band_log2=gband))
     info = M.info()
     bw = 1 << gband
     assert info["has_xband"] == 3 and info["xband_bands"] == (n_cols + bw - 1) // bw, info
@@ -721,7 +700,7 @@ def test_wide_matrix_dense_rows_fall_back_to_blocked(sm):
     rp = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int32)
     ci = np.concatenate(cols).astype(np.int32)
     va = rng.uniform(-1, 1, ci.size).astype(np.float32)
-    M = _with_env("SM_XBAND", "1", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout="bands"))
     assert M.info()["has_xband"] == 2, M.info()
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
@@ -779,17 +758,15 @@ def test_golden_spmv_cband_and_sell(sm, name):
         pytest.skip("no AddMatMat runs")
     k, n = c.s_rows, c.s_cols
 
-    def build(env):
-        def go(items):
-            if not items:
-                return _from_case(sm, c)
-            (key, v), rest = items[0], items[1:]
-            return _with_env(key, v, lambda: go(rest))
-        return go(list(env.items()))
+    H = _from_case(sm, c)          # the reference's CopyForm, then its CSR re-ingested
+    hrp, hci, hva = H.csr()
+
+    def build(opts):
+        return sm.SparseMatrix.from_csr(hrp, hci, hva, k, opts=opts)
 
     layouts = {
-        "cband": build({"SM_XBAND": "1", "SM_XBAND_KIND": "cband", "SM_BAND2_SLABS": "1"}),
-        "sell": build({"SM_XBAND": "0", "SM_SELL": "1"}),
+        "cband": build(dict(layout="cband", band_slabs=1)),
+        "sell": build(dict(layout="no_bands")),
     }
     rp, _, _ = layouts["sell"].csr()
     for lay, M in layouts.items():

@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 from gpu_util import (assert_terms_close, bits, skewed_csr, to_dev, to_host, torch_dev,
-                      uniform_csr, with_env)
+                      uniform_csr)
 
 pytestmark = pytest.mark.gpu
 
@@ -23,11 +23,11 @@ def sm():
     return sparsematrix_amd
 
 
-def _sell(sm, rp, ci, va, n_cols, relabel=None):
-    def make():
-        return with_env("SM_SELL", "1", lambda: with_env(
-            "SM_XBAND", "0", lambda: sm.SparseMatrix.from_csr(rp, ci, va, n_cols)))
-    M = with_env("SM_RELABEL", str(relabel), make) if relabel is not None else make()
+def _sell(sm, rp, ci, va, n_cols, relabel=None, **opts):
+    o = dict(layout="no_bands", **opts)
+    if relabel is not None:
+        o["relabel"] = relabel
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=o)
     info = M.info()
     assert info["sell_slices"] > 0 and info["has_xband"] == 0, info
     return M, info
@@ -82,7 +82,7 @@ def test_sell_skewed_rows_and_long_rows(sm, relabel):
 def test_sell_codebook_form(sm, skewed):
     """Values from a <= 255-entry table (the reference's uint8 ids, inf / NaN / -0.0
     among them): the slices hold column | id << 24 words (sell_codebook = 1) and give
-    the same bits as the plain column + value form (SM_SELL_CB=0) and the oracle."""
+    the same bits as the plain column + value form (sell_codebook = 0) and the oracle."""
     rng = np.random.default_rng(21)
     n_rows, n_cols = 40009, 70001
     if skewed:
@@ -96,7 +96,7 @@ def test_sell_codebook_form(sm, skewed):
     va = table[rng.integers(0, table.size, ci.size)]
     M, info = _sell(sm, rp, ci, va, n_cols, 0)
     assert info["sell_codebook"] == 1, info
-    P, pinfo = with_env("SM_SELL_CB", "0", lambda: _sell(sm, rp, ci, va, n_cols, 0))
+    P, pinfo = _sell(sm, rp, ci, va, n_cols, 0, sell_codebook=0)
     assert pinfo["sell_codebook"] == 0 and info["device_bytes"] < pinfo["device_bytes"]
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     x[0] = np.inf                       # what padding words point at
@@ -117,15 +117,14 @@ def test_sell_codebook_form(sm, skewed):
 
 @pytest.mark.parametrize("sigma,streams", [(4096, 8), (4096, 1), (1000, 3)])
 def test_sell_sort_windows(sm, sigma, streams):
-    """SELL-C-sigma layouts (SM_SELL_SIGMA rows per sort window, SM_SELL_STREAMS XCD
+    """SELL-C-sigma layouts (sell_sigma rows per sort window, sell_streams XCD
     streams of windows): the same per-row order, so the same bits as one window."""
     rng = np.random.default_rng(11)
     n_rows, n_cols = 30011, 40000
     lengths = np.minimum((rng.pareto(1.1, n_rows) * 4).astype(np.int64), 6000)
     lengths[::5] = 0
     rp, ci, va = skewed_csr(n_rows, n_cols, lengths, seed=12)
-    M, _ = with_env("SM_SELL_SIGMA", str(sigma), lambda: with_env(
-        "SM_SELL_STREAMS", str(streams), lambda: _sell(sm, rp, ci, va, n_cols, 0)))
+    M, _ = _sell(sm, rp, ci, va, n_cols, 0, sell_sigma=sigma, sell_streams=streams)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     for alpha, beta in ((1.0, 1.0), (1.3, 0.0)):
@@ -159,7 +158,7 @@ def test_sell_rmat_auto(sm):
     import sparsematrix_amd.synth as synth
     rp_d, ci_d, va_d = synth.rmat_device(20, 16, seed=4)
     n = 1 << 20
-    M = with_env("SM_XBAND", "0", lambda: sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n))
+    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands"))
     info = M.info()
     assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
     rp, ci, va = rp_d.cpu().numpy(), ci_d.cpu().numpy(), va_d.cpu().numpy()
