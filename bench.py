@@ -1,33 +1,46 @@
 #!/usr/bin/env python3
 """bench.py -- CSR SpMV effective HBM GB/s on MI355X (BASELINE.json metric).
 
-Default (N=1): BASELINE config 2 -- B is 2^20 x 2^20 with exactly 16 distinct
-uniformly random columns per row (fp32 values from a 255-entry codebook),
-y = B x + 0.5 y with the library's AUTO path (the blocked column-band kernel
-+ slab combine).  A step is one SpMV over one matrix.
-To measure HBM rather than the 256 MiB Infinity Cache, steps rotate over
-`--replicas` independent copies (matrix, x, y): 4 x 151 MB per rank.
-
-N>1 (torchrun, one process per GPU): weak scaling -- every rank owns 2^20 rows
-of a (N*2^20) x (N*2^20) matrix with global columns; a step is one RCCL
-all-gather of x (xGMI) and the local SpMV.  Steps are independent products
-(rotating replicas), so the all-gather of step k+1 runs beside the SpMV of step
-k (--no-overlap: strictly one after the other).  `value` is the sum of all
-ranks' algorithmic bytes divided by the max-over-ranks step time.
+Workloads:
+  config2 (default)  B is 2^20 x 2^20 per rank with exactly 16 distinct uniformly
+                     random columns per row (fp32 values from a 255-entry codebook),
+                     y = B x + 0.5 y with the library's AUTO layout.  N = 1: BASELINE
+                     config 2.  N > 1: weak scaling -- every rank owns 2^20 rows of an
+                     (N*2^20) x (N*2^20) matrix with global columns.
+  config5            strong scaling: 2^26 x 2^26 (`--global-rows`), 16 columns per row,
+                     rows split in N equal slices (8M rows x 64M columns per rank at
+                     N = 8).  On one GPU, `--emulate-world W` builds rank 0's slice of a
+                     W-rank job (x filled locally instead of all-gathered).
+A step is one product.  N = 1 rotates over `--replicas` independent (matrix, x, y)
+copies so the working set exceeds the 256 MiB Infinity Cache (HBM, not cache).
+N > 1 (torchrun, one process per GPU): each step is one RCCL all-gather of x over
+xGMI plus the local SpMV, through the library's C ABI (`sm_multi_*`,
+sparsematrix_amd/csrc/multi.cpp); torch.distributed (gloo) only exchanges the RCCL
+unique id and runs the barriers / max-over-ranks.  Steps are independent products,
+so the all-gather of step k+1 runs beside the SpMV of step k (`sm_multi_spmv_batch`;
+`--no-overlap`: one after the other).  `value` = the sum of all ranks' algorithmic
+bytes / the max-over-ranks time per step.
 
 Algorithmic bytes per SpMV: 8*nnz + 4*(rows+1) + 4*cols + 8*rows.
 
-Also reported, on the same JSON line:
-  roofline      the SpMV alone: algorithmic bytes / mean SpMV time vs 8 TB/s.  N=1:
-                HIP events around the replay of the captured graph of K SpMVs, on
-                the stream it runs on (so the time per SpMV includes the gaps
-                between kernels); N>1: HIP events around each sm_spmv call on its
-                stream.  `traffic` from rocprofv3 PMC
-                (profiles/traffic_<workload>_<layout>.json).
-  cpu_baseline  rank 0, N=1: the oracle's same-order CSR SpMV (C) on the same
-                matrix, over the box's CPU share (OpenMP, <= 16 threads; SURVEY
-                §8d B2) with the 1-thread figure inside; ~15 s of CPU work.
-  spmm          config 3 (same matrix, N=32 right-hand sides), GFLOP/s.
+Also on the same JSON line:
+  roofline      the dominant kernel: algorithmic bytes / SpMV time vs 8 TB/s.  N = 1:
+                HIP events around the replay of the captured graph of the K timed
+                SpMVs (per-SpMV time incl. the gaps between kernels), and the same
+                over `--replays` further replays (median / min / max reported) plus K
+                eager launches with events around each (a per-launch distribution).
+                N > 1: the local SpMV alone, K launches with events (median).
+                `traffic`: rocprofv3 PMC (profiles/traffic_<workload>_<layout>.json).
+  allgather     N > 1: the all-gather alone (K launches, events, median), and the
+                serial step (all-gather + SpMV) split by sm_multi's own events.
+  cpu_baseline  rank 0, N = 1: the oracle's same-order CSR SpMV (C, OpenMP over rows)
+                on the same matrix over every core this job may use (affinity and
+                cgroup quota, stated), with the 1-thread figure; the reference-format
+                twin (oracle/refmodel.c AddMatMat, 1 thread, what the reference runs) at
+                config 1 and 16k^2; and R-MAT over all cores.  ~30 s of CPU work.
+  spmm          config 3 (same matrix, N = 32 right-hand sides): GFLOP/s, HBM fraction,
+                traffic and MFMA utilisation from PMC (profiles/), median of 20.
+  rmat          config 4 (R-MAT scale 24) SpMV, median of 20.
 """
 from __future__ import annotations
 
@@ -44,6 +57,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3  # dense fp32 (vector = matrix rate on gfx950)
 
 
 def spmv_bytes(nnz: int, rows: int, cols: int) -> int:
@@ -65,8 +79,32 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def available_cores() -> dict:
+    """Cores this job may run on: the affinity mask, capped by the cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    use = min(aff, quota) if quota else aff
+    return {"use": use, "affinity": aff, "cgroup_quota": quota, "nproc": os.cpu_count()}
+
+
 LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband"}
 KERNELS = {"stream": "spmv_stream_kernel",
+           "sell": "spmv_sell_kernel / spmv_csell_kernel (sorted sliced-ELL)",
            "exact": "spmv_xband_kernel (exact band layout)",
            "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)",
            "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)",
@@ -75,14 +113,44 @@ KERNELS = {"stream": "spmv_stream_kernel",
                     "distributed slab combine)"}
 
 
-def load_traffic(workload: str, layout: str):
-    """HBM bytes per SpMV measured by rocprofv3 PMC (tools/pmc_traffic.py)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{workload}_{layout}.json")
+def layout_of(info: dict) -> str:
+    if info["has_xband"]:
+        return LAYOUTS[info["has_xband"]]
+    if info.get("ccsell_chunks"):
+        return "ccsell"
+    return "sell" if info["sell_slices"] else "stream"
+
+
+def load_json(name: str):
+    p = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(p):
         return None
     with open(p) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+        return json.load(f)
+
+
+def load_traffic(workload: str, layout: str):
+    """HBM bytes per SpMV measured by rocprofv3 PMC (tools/pmc_traffic.py)."""
+    d = load_json(f"traffic_{workload}_{layout}.json")
+    return d.get("hbm_bytes_per_launch") if d else None
+
+
+def stats(ms: list) -> dict:
+    a = np.asarray(ms, np.float64)
+    return {"median": round(float(np.median(a)), 5), "min": round(float(a.min()), 5),
+            "max": round(float(a.max()), 5), "n": int(a.size)}
+
+
+def event_times(torch, fn, count: int) -> list:
+    """`count` calls of fn(), a HIP event pair around each on the current stream."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(count)]
+    for i, (a, b) in enumerate(ev):
+        a.record()
+        fn(i)
+        b.record()
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
 
 
 def main():
@@ -90,11 +158,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--rows-per-rank", type=int, default=1 << 20)
+    ap.add_argument("--workload", choices=("config2", "config5"), default="config2")
+    ap.add_argument("--rows-per-rank", type=int, default=1 << 20, help="config2")
+    ap.add_argument("--global-rows", type=int, default=1 << 26, help="config5")
     ap.add_argument("--per-row", type=int, default=16)
-    ap.add_argument("--replicas", type=int, default=4)
+    ap.add_argument("--replicas", type=int, default=0, help="0: 4 (config2) / 1 (config5)")
+    ap.add_argument("--replays", type=int, default=10,
+                    help="N=1: extra graph replays for the per-SpMV time distribution")
     ap.add_argument("--algo", default="auto")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
     ap.add_argument("--spmm-n", type=int, default=32)
@@ -105,8 +177,8 @@ def main():
                     help="N=1: launch each timed step from Python instead of replaying the K "
                          "steps as one captured HIP graph")
     ap.add_argument("--emulate-world", type=int, default=0,
-                    help="development: one process builds rank 0's slice of a W-rank job "
-                         "(R rows x R*W columns, x filled locally instead of all-gathered)")
+                    help="one process builds rank 0's slice of a W-rank job (x filled locally "
+                         "instead of all-gathered)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: all-gather then SpMV per step, instead of the all-gather of "
                          "step k+1 in flight beside the SpMV of step k")
@@ -117,155 +189,243 @@ def main():
 
     import sparsematrix_amd as smd
     from sparsematrix_amd import synth
-    from sparsematrix_amd.distributed import allgather_spmv_pipelined
+    from sparsematrix_amd.distributed import MultiContext
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (use torch.distributed.run)")
-    # Development rehearsal only: SM_BENCH_DEVICE pins every rank to one GPU and
-    # SM_BENCH_BACKEND=gloo replaces RCCL, so the N>1 code path can run on a one-GPU box.
-    dev_index = int(os.environ.get("SM_BENCH_DEVICE", local_rank))
+    # Development rehearsal of the N > 1 bookkeeping on a one-GPU box: SM_BENCH_REHEARSE=1
+    # puts every rank on GPU 0 and moves x over the gloo group (RCCL refuses two ranks
+    # on one GPU); the numbers are not a measurement.
+    rehearse = world > 1 and os.environ.get("SM_BENCH_REHEARSE") == "1"
+    dev_index = 0 if rehearse else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
-        backend = os.environ.get("SM_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+    if world > 1:   # control plane only: unique id, barriers, max over ranks
+        dist.init_process_group("gloo")
     smd.load()
 
-    if args.replicas < 1:
-        raise SystemExit("--replicas must be >= 1")
-    if world > 1 and not args.no_overlap and args.replicas < 2:
-        raise SystemExit("--gpus N>1 overlaps the all-gather of step k+1 with the SpMV of step k, "
-                         "which needs >= 2 replicas (distinct x buffers); use --replicas 2+ or "
-                         "--no-overlap")
-    R = args.rows_per_rank
     emu = args.emulate_world if world == 1 and args.emulate_world > 1 else 1
-    C = R * world * emu                    # global columns (= global rows)
+    parts = world * emu
+    if args.workload == "config2":
+        R = args.rows_per_rank
+        C = R * parts                       # global columns (= global rows)
+        seed0 = 2
+        replicas = args.replicas or 4
+    else:
+        if args.global_rows % parts:
+            raise SystemExit("--global-rows must split evenly over the ranks")
+        C = args.global_rows
+        R = C // parts
+        seed0 = 5
+        replicas = args.replicas or 1
     per = args.per_row
+    if world > 1 and C % world:
+        raise SystemExit("the columns must split evenly over the ranks (one all-gather)")
+
+    t_build0 = time.perf_counter()
     reps = []
-    for k in range(args.replicas):
-        seed = 2 + 1000 * k + 7919 * rank
+    for k in range(replicas):
+        seed = seed0 + 1000 * k + 7919 * rank
         rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
         M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index)
         g = torch.Generator(device=dev).manual_seed(seed + 1)
-        x_local = torch.rand(R, generator=g, device=dev) * 2 - 1
-        x_full = (torch.empty(C, device=dev) if world > 1 else
+        x_local = torch.rand(C // world if world > 1 else R, generator=g, device=dev) * 2 - 1
+        x_full = (None if world > 1 else
                   torch.rand(C, generator=g, device=dev) * 2 - 1 if emu > 1 else x_local)
+        if world == 1 and emu == 1 and args.workload == "config5":
+            x_full = torch.rand(C, generator=g, device=dev) * 2 - 1
         y = torch.rand(R, generator=g, device=dev) * 2 - 1
-        reps.append(dict(M=M, rp=rp, ci=ci, va=va, x_local=x_local, x_full=x_full, y=y))
-        if k:
-            del rp, ci, va
+        reps.append(dict(M=M, rp=rp if k == 0 else None, ci=ci if k == 0 else None,
+                         va=va if k == 0 else None, x_local=x_local, x_full=x_full, y=y))
+        del rp, ci, va
+    build_s = time.perf_counter() - t_build0
     nnz = R * per
     bytes_rank = spmv_bytes(nnz, R, C)
     torch.cuda.synchronize()
+    info = reps[0]["M"].info()
+    layout = layout_of(info) if args.algo in ("auto", "xband", "sell") else args.algo
+    workload = (f"spmv_{R}x{C}_{per}_per_row" if args.workload == "config2"
+                else f"config5_{C}x{C}_{per}_per_row_rank0of{parts}")
 
-    def step(i, ev=None):
-        r = reps[i % len(reps)]
-        if world > 1:
-            dist.all_gather_into_tensor(r["x_full"], r["x_local"])
-        if ev is not None:
-            ev[0].record()
-        r["M"].spmv(r["x_full"], r["y"], 1.0, 0.5, algo=args.algo)
-        if ev is not None:
-            ev[1].record()
+    ctx = None
+    path = None
+    nccl_group = None
+    fallback = None
+    if world > 1:
+        uid = torch.zeros(128, dtype=torch.uint8)
+        err = None
+        if rank == 0:
+            try:
+                uid = torch.frombuffer(bytearray(MultiContext.unique_id()), dtype=torch.uint8).clone()
+            except Exception as exc:  # noqa: BLE001
+                err = exc
+        dist.broadcast(uid, 0)
+        if rehearse:
+            err = RuntimeError("rehearsal: every rank on one GPU")
+        elif err is None and int(uid.sum()) != 0:
+            try:
+                ctx = MultiContext(reps[0]["M"], world, rank, bytes(uid.numpy().tobytes()))
+            except Exception as exc:  # noqa: BLE001
+                err = exc
+        ok = torch.tensor([1 if ctx is not None else 0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            path = "sm_multi_spmv_batch (C ABI, ncclAllGather)" if not args.no_overlap \
+                else "sm_multi_spmv (C ABI, ncclAllGather)"
+        else:
+            # The C-ABI context failed on some rank: the same data path through torch's
+            # RCCL group (all_gather_into_tensor + the local SpMV), reported as such.
+            if ctx is not None:
+                ctx.close()
+                ctx = None
+            fallback = f"{type(err).__name__}: {err}"[:300] if err else "failed on another rank"
+            nccl_group = None if rehearse else dist.new_group(backend="nccl")
+            for r in reps:
+                r["x_full"] = torch.empty(C, device=dev)
+            path = "torch.distributed all_gather_into_tensor (RCCL; sm_multi fallback)"
 
-    # N > 1, default: steps are independent products (rotating replicas), so the
-    # all-gather of step k+1 runs beside the SpMV of step k (distributed.py,
-    # allgather_spmv_pipelined) -- still one all-gather per step, no other collective.
     overlap = world > 1 and not args.no_overlap
 
-    def products(start, count, evs=None):
-        for j in range(count):
-            r = reps[(start + j) % len(reps)]
+    def run_steps(start: int, count: int):
+        """`count` products from step `start` on (replicas rotate)."""
+        idx = [(start + j) % len(reps) for j in range(count)]
+        if world == 1:
+            for i in idx:
+                r = reps[i]
+                r["M"].spmv(r["x_full"], r["y"], 1.0, 0.5, algo=args.algo)
+        elif ctx is None:   # fallback: torch's RCCL all-gather, then the local SpMV
+            from sparsematrix_amd.distributed import allgather_spmv_pipelined
 
-            def local(xf, yl, r=r, e=(evs[j] if evs is not None else None)):
-                if e is not None:
-                    e[0].record()
-                r["M"].spmv(xf, yl, 1.0, 0.5, algo=args.algo)
-                if e is not None:
-                    e[1].record()
-            yield (local, r["x_local"], r["x_full"], r["y"])
+            def products():
+                for i in idx:
+                    r = reps[i]
+                    yield (lambda xf, yl, r=r: r["M"].spmv(xf, yl, 1.0, 0.5, algo=args.algo),
+                           r["x_local"], r["x_full"], r["y"])
+            if overlap and len(reps) > 1:
+                allgather_spmv_pipelined(products(), group=nccl_group)
+            else:
+                for f, xl, xf, yl in products():
+                    dist.all_gather_into_tensor(xf, xl, group=nccl_group)
+                    f(xf, yl)
+        elif overlap:
+            ctx.spmv_batch([reps[i]["x_local"] for i in idx], [reps[i]["y"] for i in idx],
+                           1.0, 0.5, algo=args.algo, mats=[reps[i]["M"] for i in idx])
+        else:
+            for i in idx:   # one product per call: its all-gather, then its SpMV
+                r = reps[i]
+                ctx.spmv_batch([r["x_local"]], [r["y"]], 1.0, 0.5, algo=args.algo, mats=[r["M"]])
 
-    if overlap:
-        allgather_spmv_pipelined(products(0, args.warmup))
-    else:
-        for i in range(args.warmup):
-            step(i)
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     # N = 1: the K timed SpMVs are captured once into a HIP graph (capturing runs
-    # nothing) and replayed as one launch, so the timed region holds the kernels
-    # back to back with no Python / ctypes / per-call launch cost between them; HIP
-    # events bracket the whole region on the stream the kernels run on.  N > 1:
-    # every step (RCCL all-gather + SpMV) is launched eagerly, with events around
-    # each SpMV.
+    # nothing) and replayed as one launch, so the timed region holds the kernels back
+    # to back with no Python / ctypes / per-call launch cost between them.
     use_graph = world == 1 and not args.no_graph
     graph = None
     if use_graph:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            for i in range(args.steps):
-                step(args.warmup + i)
+            run_steps(args.warmup, args.steps)
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
     if use_graph:
-        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-        t0 = time.perf_counter()
-        events[0][0].record()
         graph.replay()
-        events[0][1].record()
     else:
-        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(args.steps)]
-        t0 = time.perf_counter()
-        if overlap:
-            allgather_spmv_pipelined(products(args.warmup, args.steps, events))
-        else:
-            for i in range(args.steps):
-                step(args.warmup + i, events[i])
+        run_steps(args.warmup, args.steps)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in events]
-    if use_graph:   # one region of K SpMVs: per-SpMV time incl. the gaps between kernels
-        kern_ms = [kern_ms[0] / args.steps]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    region_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = bytes_rank * world / (elapsed / args.steps) / 1e9
-    kmean = float(np.mean(kern_ms))
-    kmed = float(np.median(kern_ms))
-    achieved = bytes_rank / (kmean * 1e-3) / 1e9
-    workload = f"spmv_{R}x{C}_{per}_per_row"
-    info = reps[0]["M"].info()
-    layout = LAYOUTS[info["has_xband"]] if args.algo in ("auto", "xband") else "stream"
+
+    # ---- distributions, outside the timed region ----------------------------------
+    dist_info = {}
+    if use_graph:
+        per_replay = []
+        for _ in range(max(1, args.replays)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            graph.replay()
+            b.record()
+            torch.cuda.synchronize()
+            per_replay.append(a.elapsed_time(b) / args.steps)
+        dist_info["graph_replay_ms_per_spmv"] = stats([region_ms / args.steps] + per_replay)
+        kern_ms = float(np.median([region_ms / args.steps] + per_replay))
+    xs_local = None
+    if world == 1:
+        def one(i):
+            r = reps[i % len(reps)]
+            r["M"].spmv(r["x_full"], r["y"], 1.0, 0.5, algo=args.algo)
+        eager = event_times(torch, one, args.steps)
+        dist_info["eager_launch_ms"] = stats(eager)
+        if not use_graph:
+            kern_ms = float(np.median(eager))
+    else:
+        # the all-gather alone, the local SpMV alone, and the serial step split by events
+        x_tmp = torch.empty(C, device=dev)
+        if ctx is not None:
+            ag = event_times(torch, lambda i: ctx.allgather(reps[i % len(reps)]["x_local"]), args.steps)
+        else:
+            ag = event_times(torch, lambda i: dist.all_gather_into_tensor(
+                x_tmp, reps[i % len(reps)]["x_local"], group=nccl_group), args.steps)
+
+        def local(i):
+            r = reps[i % len(reps)]
+            r["M"].spmv(x_tmp, r["y"], 1.0, 0.5, algo=args.algo)
+        loc = event_times(torch, local, args.steps)
+        dist_info["allgather_ms"] = stats(ag)
+        dist_info["allgather_bytes_per_rank"] = 4 * C
+        dist_info["allgather_gbs_per_rank"] = round(4 * C / (float(np.median(ag)) * 1e-3) / 1e9, 1)
+        dist_info["local_spmv_ms"] = stats(loc)
+        if ctx is not None:
+            ctx.set_timing(True)
+            split = []
+            for i in range(args.steps):   # the context's own matrix (replica 0)
+                ctx.spmv(reps[0]["x_local"], reps[0]["y"], 1.0, 0.5, algo=args.algo)
+                split.append(ctx.last_times())
+            ctx.set_timing(False)
+            dist_info["serial_step_split_ms"] = {"allgather": stats([s[0] for s in split]),
+                                                "spmv": stats([s[1] for s in split])}
+        if fallback:
+            dist_info["sm_multi_fallback"] = fallback
+        kern_ms = float(np.median(loc))
+        del x_tmp
+    achieved = bytes_rank / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(workload, layout) if world == 1 else None
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
             "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
             "traffic": traffic,
             # the HBM bytes the kernel really moves (PMC) over its measured time
-            "traffic_frac": (round(traffic / (kmean * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+            "traffic_frac": (round(traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
                              if traffic else None),
             "traffic_source": (f"profiles/traffic_{workload}_{layout}.json (rocprofv3 PMC, "
                                "FETCH_SIZE x calibration + WRITE_SIZE)" if traffic else None),
-            "kernel": KERNELS[layout], "layout": layout,
+            "kernel": KERNELS.get(layout, layout), "layout": layout,
             "xband_slabs": info["xband_slabs"], "xband_block_rows": info["xband_block_rows"],
-            "kernel_ms_mean": round(kmean, 5), "kernel_ms_median": round(kmed, 5),
-            "alg_bytes_per_launch": bytes_rank}
+            "kernel_ms": round(kern_ms, 5),
+            "kernel_ms_source": ("median over graph replays (per SpMV incl. inter-kernel gaps)"
+                                 if use_graph else "median of per-launch HIP events"),
+            "alg_bytes_per_launch": bytes_rank, "distribution": dist_info}
 
-    # ---- SpMM (config 3) on replica 0, same ranks ---------------------------------
+    # ---- SpMM (config 3) on replica 0 -----------------------------------------------
     spmm = None
-    if not args.no_spmm:
+    if not args.no_spmm and args.workload == "config2":
         N = args.spmm_n
         r0 = reps[0]
         g = torch.Generator(device=dev).manual_seed(3)
@@ -274,28 +434,33 @@ def main():
         for _ in range(3):
             r0["M"].spmm(X, Y, 1.0, 0.5)
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(10)]
-        for a, b in ev:
-            a.record()
-            r0["M"].spmm(X, Y, 1.0, 0.5)
-            b.record()
-        torch.cuda.synchronize()
-        sm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        sm_ms_list = event_times(torch, lambda i: r0["M"].spmm(X, Y, 1.0, 0.5), 20)
+        sm_ms = float(np.median(sm_ms_list))
         sb = spmm_bytes(nnz, R, C, N)
-        spmm = {"n_rhs": N, "ms": round(sm_ms, 4),
+        swl = f"spmm_{R}x{C}_{per}_per_row_n{N}"
+        st = load_json(f"traffic_{swl}_rowpanel2.json")
+        mf = load_json(f"mfma_{swl}_rowpanel2.json")
+        spmm = {"n_rhs": N, "ms": round(sm_ms, 4), "ms_stats": stats(sm_ms_list),
                 "gflops": round(2.0 * nnz * N / (sm_ms * 1e-3) / 1e9, 1),
-                "hbm_gbs": round(sb / (sm_ms * 1e-3) / 1e9, 1),
+                "flop_frac": round(2.0 * nnz * N / (sm_ms * 1e-3) / 1e12 / PEAK_F32_TFLOPS, 4),
+                "alg_bytes": sb, "hbm_gbs": round(sb / (sm_ms * 1e-3) / 1e9, 1),
                 "hbm_frac": round(sb / (sm_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                "kernel": "spmm_rowpanel2_kernel<8>", "mfma": "not used (fp32 SpMM at "
-                "~2 flop/B is HBM/gather bound; see DESIGN.md)"}
+                "traffic": st.get("hbm_bytes_per_launch") if st else None,
+                "traffic_source": f"profiles/traffic_{swl}_rowpanel2.json" if st else None,
+                "mfma_util": mf.get("mfma_util") if mf else None,
+                "mfma_insts": mf.get("mfma_insts") if mf else None,
+                "mfma_source": (f"profiles/mfma_{swl}_rowpanel2.json (rocprofv3 "
+                                "SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, SQ_INSTS_VALU_MFMA_F32)"
+                                if mf else None),
+                "kernel": "spmm_rowpanel2_kernel<8> (fp32 VALU; MFMA not used: ~2 flop/B, "
+                          "DESIGN.md §3.5)"}
         del X, Y
 
-    # ---- R-MAT (config 4) on rank 0 at N = 1: AUTO on a Graph500 graph --------------
+    # ---- R-MAT (config 4) on rank 0 at N = 1 ----------------------------------------
     rmat = None
-    if world == 1 and rank == 0 and not args.no_rmat:
+    rmat_host = None
+    if world == 1 and emu == 1 and rank == 0 and not args.no_rmat and args.workload == "config2":
         try:   # a failure here must not cost the config-2 line
-            from sparsematrix_amd import synth
             torch.cuda.synchronize()
             t_b = time.perf_counter()
             rrp, rci, rva = synth.rmat_device(args.rmat_scale, 16, seed=4)
@@ -310,28 +475,24 @@ def main():
             for _ in range(3):
                 RM.spmv(rx, ry, 1.0, 0.5)
             torch.cuda.synchronize()
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(10)]
-            for a, b in ev:
-                a.record()
-                RM.spmv(rx, ry, 1.0, 0.5)
-                b.record()
-            torch.cuda.synchronize()
-            r_ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+            r_list = event_times(torch, lambda i: RM.spmv(rx, ry, 1.0, 0.5), 20)
+            r_ms = float(np.median(r_list))
             rnnz = int(rci.numel())
             rb = spmv_bytes(rnnz, rn, rn)
-            kind = ("band kind %d" % rinfo["has_xband"] if rinfo["has_xband"]
-                    else ("sorted sliced-ELL (%s) + long-row segments"
-                          % ("4-byte column|codebook-id words" if rinfo["sell_codebook"] else "column + value")
-                          if rinfo["sell_slices"] else "stream"))
+            lay = layout_of(rinfo)
             rmat = {"scale": args.rmat_scale, "rows": rn, "nnz": rnnz,
                     "max_row_nnz": rinfo["max_row_nnz"], "ms": round(r_ms, 4),
-                    "alg_bytes": rb, "gbs": round(rb / (r_ms * 1e-3) / 1e9, 1),
+                    "ms_stats": stats(r_list), "alg_bytes": rb,
+                    "gbs": round(rb / (r_ms * 1e-3) / 1e9, 1),
                     "frac": round(rb / (r_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                    "kernel": kind + (", relabeled columns" if rinfo["col_relabel"] else ""),
+                    "layout": lay, "col_relabel": rinfo["col_relabel"],
+                    "sell_codebook": rinfo["sell_codebook"],
                     "generate_s": round(t_g - t_b, 1), "build_s": round(t_c - t_g, 1),
-                    "timing": "HIP events around each SpMV (median of 10, eager launches, "
-                              "x permutation and finalize included)"}
+                    "timing": "HIP events around each SpMV (median of 20 eager launches, x "
+                              "permutation and finalize included)"}
+            if not args.no_cpu:
+                rmat_host = (rrp.cpu().numpy(), rci.cpu().numpy(), rva.cpu().numpy(),
+                             rx.cpu().numpy(), ry.cpu().numpy(), rb)
             del RM, rrp, rci, rva, rx, ry
             torch.cuda.empty_cache()
         except Exception as exc:  # noqa: BLE001
@@ -339,60 +500,105 @@ def main():
 
     # ---- CPU baseline (rank 0, N = 1) --------------------------------------------
     cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu:
-        import oracle
-        r0 = reps[0]
-        rp = r0["rp"].cpu().numpy()
-        ci = r0["ci"].cpu().numpy()
-        va = r0["va"].cpu().numpy()
-        x = r0["x_full"].cpu().numpy()
-        y0 = r0["y"].cpu().numpy()
-        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
-
-        def timed(fn, budget):
-            fn()                                                # warm
-            n_rep, t_cpu = 0, 0.0
-            while t_cpu < budget and n_rep < 5000:
-                c0 = time.perf_counter()
-                fn()
-                t_cpu += time.perf_counter() - c0
-                n_rep += 1
-            return n_rep, t_cpu
-
-        n1, t1 = timed(lambda: oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5), args.cpu_seconds)
-        nm, tm = timed(lambda: oracle.csr_spmv_mt(rp, ci, va, x, y0, 1.0, 0.5, threads=threads),
-                       args.cpu_seconds / 2)
-        cpu = {"value": round(bytes_rank * nm / tm / 1e9, 3), "unit": "GB/s", "cores": threads,
-               "kind": "port",
-               "sample": f"oracle same-order CSR SpMV (C, OpenMP over rows, {threads} threads) on "
-                         f"the full config-2 matrix (replica 0), {nm} reps in {tm:.1f} s",
-               "ms_per_spmv": round(1e3 * tm / nm, 3),
-               "single_thread": {"value": round(bytes_rank * n1 / t1 / 1e9, 3), "unit": "GB/s",
-                                 "cores": 1, "ms_per_spmv": round(1e3 * t1 / n1, 3),
-                                 "sample": f"{n1} reps in {t1:.1f} s (the reference kernel is "
-                                           f"single-threaded)"},
-               "cpu": cpu_model(),
-               "nproc": os.cpu_count()}
+    if world == 1 and rank == 0 and not args.no_cpu and reps[0]["rp"] is not None:
+        cpu = cpu_baseline(args, reps[0], bytes_rank, rmat_host)
 
     if rank == 0:
         line = {
             "metric": "CSR SpMV effective HBM GB/s", "value": round(value, 1), "unit": "GB/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+            "scaling": "weak" if args.workload == "config2" else "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": workload, "rows_per_rank": R, "cols": C, "nnz_per_rank": nnz,
-                       "per_row": per, "replicas": args.replicas, "algo": args.algo,
+                       "per_row": per, "replicas": replicas, "algo": args.algo,
                        "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
+                       "build_s": round(build_s, 1),
                        "parallelism": f"row-partition x{world}" + (
-                           ", RCCL all-gather(x)" + (" of step k+1 overlapped with SpMV k"
-                                                     if overlap else "") if world > 1 else ""),
+                           f", {path}" + (": all-gather of step k+1 beside SpMV k"
+                                          if overlap else "") if world > 1 else ""),
                        **({"emulate_world": emu} if emu > 1 else {})},
             "roofline": roof, "cpu_baseline": cpu, "spmm": spmm, "rmat": rmat,
         }
         print(json.dumps(line), flush=True)
+    if ctx is not None:
+        ctx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def cpu_baseline(args, r0, bytes_rank, rmat_host):
+    """B2 (same-order CSR, all cores + 1 thread), B1 (the reference-format
+    twin, 1 thread, config 1 and 16k^2), B2 on R-MAT.  The oracle is the checker and
+    this CPU baseline only; nothing of it runs in the timed GPU region."""
+    import oracle
+    from sparsematrix_amd import synth
+    rp = r0["rp"].cpu().numpy()
+    ci = r0["ci"].cpu().numpy()
+    va = r0["va"].cpu().numpy()
+    x = r0["x_full"].cpu().numpy()
+    y0 = r0["y"].cpu().numpy()
+    cores = available_cores()
+    threads = cores["use"]
+
+    def timed(fn, budget):
+        fn()                                                # warm
+        n_rep, t_cpu = 0, 0.0
+        while t_cpu < budget and n_rep < 5000:
+            c0 = time.perf_counter()
+            fn()
+            t_cpu += time.perf_counter() - c0
+            n_rep += 1
+        return n_rep, t_cpu
+
+    sec = args.cpu_seconds
+    n1, t1 = timed(lambda: oracle.csr_spmv(rp, ci, va, x, y0, 1.0, 0.5), sec)
+    nm, tm = timed(lambda: oracle.csr_spmv_mt(rp, ci, va, x, y0, 1.0, 0.5, threads=threads), sec / 2)
+    out = {"value": round(bytes_rank * nm / tm / 1e9, 3), "unit": "GB/s", "cores": threads,
+           "kind": "port",
+           "sample": f"oracle same-order CSR SpMV (C, OpenMP over rows, {threads} threads = every "
+                     f"core this job may use) on the full config-2 matrix (replica 0), {nm} reps "
+                     f"in {tm:.1f} s",
+           "ms_per_spmv": round(1e3 * tm / nm, 3),
+           "cores_detail": cores,
+           "single_thread": {"value": round(bytes_rank * n1 / t1 / 1e9, 3), "unit": "GB/s",
+                             "cores": 1, "ms_per_spmv": round(1e3 * t1 / n1, 3),
+                             "sample": f"{n1} reps in {t1:.1f} s"},
+           "cpu": cpu_model()}
+    # B1: the reference-format twin (uint8 deltas + ids + 256-column panels, the
+    # reference's AddMatMat op order, 1 thread): config 1 and 16k^2 at 0.1 %.
+    b1 = {}
+    table = synth.codebook()
+    for name, n, dens, seed in (("config1_1024x1024_1pct", 1024, 0.01, 1),
+                                ("16384x16384_0.1pct", 16384, 0.001, 6)):
+        rng = np.random.default_rng(seed)
+        live = rng.random((n, n)) < dens
+        dm = np.where(live, rng.integers(0, 255, (n, n)), 255).astype(np.uint8)
+        t_e = time.perf_counter()
+        ref = oracle.RefModel(dm, n, n, n, table, 255, trans=True)
+        enc_s = time.perf_counter() - t_e
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        c = rng.uniform(-1, 1, n).astype(np.float32)
+        k, t_r = timed(lambda: ref.add_mat_mat(a, 1, n, c, n, 1.0, 0.5), min(2.0, sec / 4))
+        nz = ref.nnz()
+        ms = 1e3 * t_r / k
+        b1[name] = {"ms": round(ms, 4), "nnz": int(nz),
+                    "gbs": round(spmv_bytes(nz, n, n) / (ms * 1e-3) / 1e9, 3),
+                    "encode_s": round(enc_s, 3), "reps": k}
+        del dm, live, ref
+    out["b1_reference_format_1thread"] = {
+        "kind": "port", "cores": 1, "cases": b1,
+        "sample": "oracle/refmodel.c AddMatMat on the reference's own format (m = 1, alpha 1, "
+                  "beta 0.5), B = dense uint8 id matrix (Trans), codebook of 255 floats"}
+    if rmat_host is not None:
+        rrp, rci, rva, rx, ry, rb = rmat_host
+        k, t_r = timed(lambda: oracle.csr_spmv_mt(rrp, rci, rva, rx, ry, 1.0, 0.5, threads=threads),
+                       sec / 2)
+        out["rmat"] = {"ms_per_spmv": round(1e3 * t_r / k, 3), "cores": threads,
+                       "gbs": round(rb * k / t_r / 1e9, 3), "reps": k,
+                       "sample": "same-order CSR SpMV over the R-MAT scale-24 CSR"}
+    return out
 
 
 if __name__ == "__main__":

@@ -321,12 +321,14 @@ SM_API sm_status sm_multi_spmv(sm_multi *mc, float alpha, const float *x_local, 
 SM_API sm_status sm_multi_spmm(sm_multi *mc, int32_t n_rhs, float alpha, const float *X_local,
                                float beta, float *Y_local, int64_t ldy, sm_algo algo,
                                sm_stream stream);
-/* `count` independent products x_local[i] -> y_local[i]: the all-gather of product i+1
- * runs on the context's own stream beside the SpMV of product i on `stream` (two
- * gather buffers alternate); still one all-gather per product.  Returns with all of
- * the batch ordered before later work on `stream`. */
-SM_API sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, float alpha,
-                                     const float *const *x_local, float beta,
+/* `count` independent products y_local[i] = alpha * B_i * x + beta * y_local[i], x the
+ * all-gather of x_local[i], B_i = locals[i] (NULL: the context's matrix; others must
+ * have the same global columns and device): the all-gather of product i+1 runs on the
+ * context's own stream beside the SpMV of product i on `stream` (two gather buffers
+ * alternate); still one all-gather per product.  Returns with the whole batch ordered
+ * before later work on `stream`. */
+SM_API sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, const sm_matrix *const *locals,
+                                     float alpha, const float *const *x_local, float beta,
                                      float *const *y_local, sm_algo algo, sm_stream stream);
 /* The all-gather alone (n_rhs = 1 for x), into the context's buffer; *x_full (optional)
  * receives its device address, valid until the next call on the context. */

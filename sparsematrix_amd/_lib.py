@@ -149,8 +149,8 @@ def _declare(L):
         "sm_multi_destroy": ([_vp], None),
         "sm_multi_spmv": ([_vp, _f32, _vp, _f32, _vp, C.c_int, _vp], C.c_int),
         "sm_multi_spmm": ([_vp, _i32, _f32, _vp, _f32, _vp, _i64, C.c_int, _vp], C.c_int),
-        "sm_multi_spmv_batch": ([_vp, _i32, _f32, C.POINTER(_vp), _f32, C.POINTER(_vp), C.c_int,
-                                 _vp], C.c_int),
+        "sm_multi_spmv_batch": ([_vp, _i32, C.POINTER(_vp), _f32, C.POINTER(_vp), _f32,
+                                 C.POINTER(_vp), C.c_int, _vp], C.c_int),
         "sm_multi_allgather": ([_vp, _vp, _i32, _vp, C.POINTER(_vp)], C.c_int),
         "sm_multi_set_timing": ([_vp, _i32], C.c_int),
         "sm_multi_last_times": ([_vp, C.POINTER(_f32), C.POINTER(_f32)], C.c_int),

@@ -323,11 +323,19 @@ sm_status sm_multi_spmm(sm_multi *mc, int32_t n_rhs, float alpha, const float *X
     return SM_OK;
 }
 
-sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, float alpha, const float *const *x_local,
-                              float beta, float *const *y_local, sm_algo algo, sm_stream stream) {
+sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, const sm_matrix *const *locals,
+                              float alpha, const float *const *x_local, float beta,
+                              float *const *y_local, sm_algo algo, sm_stream stream) {
     if (!mc) return mfail(SM_ERR_INVALID_ARG, "null context");
     if (count < 0 || (count > 0 && (!x_local || !y_local)))
         return mfail(SM_ERR_INVALID_ARG, "bad batch arguments");
+    for (int32_t i = 0; locals && i < count; ++i) {   // other matrices: same rank, same columns
+        sm_info li;
+        if (!locals[i] || sm_get_info(locals[i], &li) != SM_OK || li.n_cols != mc->n_cols ||
+            li.device != mc->device)
+            return mfail(SM_ERR_INVALID_ARG, "batch matrix %d: needs %lld global columns on device %d",
+                         i, (long long)mc->n_cols, mc->device);
+    }
     if (count == 0) return SM_OK;
     std::lock_guard<std::mutex> lk(mc->mu);
     DevScope g(mc->device);
@@ -357,7 +365,8 @@ sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, float alpha, const fl
             st = hip_mfail(e, "sm_multi_spmv_batch");
             break;
         }
-        st = sm_spmv(mc->local, alpha, mc->xbuf[b], beta, y_local[i], algo, stream);
+        st = sm_spmv(locals ? locals[i] : mc->local, alpha, mc->xbuf[b], beta, y_local[i], algo,
+                     stream);
         if (st != SM_OK) {
             st = mfail(st, "local SpMV: %s", sm_last_error());
             break;

@@ -162,15 +162,18 @@ class MultiContext:
                          "sm_multi_spmm")
         return Y_local
 
-    def spmv_batch(self, xs, ys, alpha=1.0, beta=1.0, algo="auto", stream=None):
+    def spmv_batch(self, xs, ys, alpha=1.0, beta=1.0, algo="auto", stream=None, mats=None):
+        """Independent products ys[i] = alpha * B_i * allgather(xs[i]) + beta * ys[i],
+        B_i = mats[i] (default: the context's matrix); all-gather i+1 beside SpMV i."""
         import ctypes as C
         from . import _lib
         from .sparse_matrix import _algo
         n = len(xs)
         xa = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
         ya = (C.c_void_p * n)(*[y.data_ptr() for y in ys])
-        _lib.check_multi(self._L.sm_multi_spmv_batch(self._h, n, alpha, xa, beta, ya, _algo(algo),
-                                                     self._stream(ys[0], stream)),
+        ma = (C.c_void_p * n)(*[m._require().value for m in mats]) if mats is not None else None
+        _lib.check_multi(self._L.sm_multi_spmv_batch(self._h, n, ma, alpha, xa, beta, ya,
+                                                     _algo(algo), self._stream(ys[0], stream)),
                          "sm_multi_spmv_batch")
 
     def allgather(self, x_local, n_rhs: int = 1, stream=None) -> int:
