@@ -114,7 +114,8 @@ typedef struct sm_info {
     int32_t xband_slab_cols;    /* columns per slab (slab s = [s*c, (s+1)*c))   */
     int64_t sell_slices;        /* sorted sliced-ELL slices of 64 rows (0: not built) */
     int32_t sell_codebook;      /* 1: the slices hold 4-byte column | codebook-id words */
-    int32_t reserved0;
+    int32_t ccsell_chunks;      /* column chunks of the column-chunked sliced ELL (0: not built);
+                                   it serves SpMV when built (AUTO, SELL): every row bit-identical */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -194,6 +195,9 @@ typedef struct sm_build_opts {
     int64_t sell_sigma;        /* sort rows by length within windows of this many rows, 0 = globally */
     int32_t relabel;           /* column relabeling by degree: -1 auto, 0 never, 1 always */
     int32_t tile_nnz;          /* stream-kernel tile: 1024/2048/4096/8192, 0 = auto   */
+    int32_t ccsell;            /* column-chunked sliced-ELL (wide x): -1 auto, 0 never, 1 always
+                                  (where no band layout is built and it applies)       */
+    int32_t ccsell_chunk_log2; /* its column chunk, log2 columns (8..24), 0 = 20 (4 MiB of x) */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);

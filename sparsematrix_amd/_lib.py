@@ -63,7 +63,7 @@ class SmInfo(C.Structure):
         ("max_row_nnz", C.c_int32), ("has_xband", C.c_int32), ("xband_blocks", C.c_int32),
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
-        ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("reserved0", C.c_int32),
+        ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("ccsell_chunks", C.c_int32),
     ]
 
 
@@ -78,6 +78,7 @@ class SmBuildOpts(C.Structure):
         ("band_tall", C.c_int32), ("gather_band_log2", C.c_int32), ("sell", C.c_int32),
         ("sell_codebook", C.c_int32), ("sell_max_len", C.c_int32), ("sell_streams", C.c_int32),
         ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
+        ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32),
     ]
 
 

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "ccsell.h"
 #include "encode.h"
 #include "sm_internal.h"
 #include "sell.h"
@@ -100,6 +101,13 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.sell.d_long_rows);
     (void)hipFree(m->plan.sell.d_long_ptr);
     (void)hipFree(m->plan.sell.d_partials);
+    (void)hipFree(m->plan.cc.d_off);
+    (void)hipFree(m->plan.cc.d_len);
+    (void)hipFree(m->plan.cc.d_row);
+    (void)hipFree(m->plan.cc.d_row_len);
+    (void)hipFree(m->plan.cc.d_word);
+    (void)hipFree(m->plan.cc.d_val);
+    (void)hipFree(m->plan.cc.d_table);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
     if (m->scratch_ready) (void)hipEventDestroy(m->scratch_ready);
@@ -150,6 +158,8 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.sell_sigma = d.sell_sigma;
         r.relabel = d.relabel;
         r.tile_nnz = d.tile_nnz;
+        r.ccsell = d.ccsell;
+        r.ccsell_chunk_log2 = d.ccsell_chunk_log2;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -167,6 +177,8 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     if (const char *e = dev_env("SM_SELL_SIGMA")) r.sell_sigma = atoll(e);
     if (const char *e = dev_env("SM_SELL_STREAMS")) r.sell_streams = atoi(e);
     if (const char *e = dev_env("SM_TILE_NNZ")) r.tile_nnz = atoi(e);
+    if (const char *e = dev_env("SM_CCSELL")) r.ccsell = atoi(e);
+    if (const char *e = dev_env("SM_CCSELL_CHUNK")) r.ccsell_chunk_log2 = atoi(e);
     return r;
 }
 
@@ -186,6 +198,8 @@ sm_status check_opts(const sm_build_opts *o) {
         return fail(SM_ERR_INVALID_ARG, "tile_nnz must be 0, 1024, 2048, 4096 or 8192");
     if (r.sell_max_len < 0 || r.sell_streams < 0 || r.sell_sigma < 0)
         return fail(SM_ERR_INVALID_ARG, "negative sell option");
+    if (r.ccsell_chunk_log2 != 0 && (r.ccsell_chunk_log2 < 8 || r.ccsell_chunk_log2 > 24))
+        return fail(SM_ERR_INVALID_ARG, "ccsell_chunk_log2 must be 0 or 8..24");
     return SM_OK;
 }
 
@@ -451,7 +465,7 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
 // reference's order (the stream kernel: rows up to 64).
 bool want_sell(const sm_matrix *m) {
     if (m->opts.sell == 0) return false;
-    return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0;
+    return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0 && m->plan.cc.n_slices == 0;
 }
 
 sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
@@ -520,6 +534,63 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
         if (!cb) SM_TRY_HIP(hipMemcpy(d.d_val, sh.val.data(), (size_t)sh.padded * 4, hipMemcpyHostToDevice));
     }
     d.n_slices = sh.n_slices;
+    return SM_OK;
+}
+
+// Column-chunked sorted sliced-ELL (ccsell.h, kernels_ccsell.hip):
+// AUTO builds it instead of the sliced ELL when x is far larger than an XCD's L2
+// (>= 2^23 columns = 32 MiB, 8 L2s' worth) and no band layout or relabeling serves
+// the matrix -- a row-ordered ELL would gather every term's x from the Infinity Cache
+// or HBM.  It declines (and the sliced ELL serves) when one row has more than 2048
+// terms inside one column chunk.  ccsell = 0 / 1 never / always tries it.
+bool want_ccsell(const sm_matrix *m) {
+    if (m->opts.ccsell == 0 || m->opts.sell == 0) return false;
+    if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0 || m->plan.n_relabel > 0)
+        return false;
+    return m->opts.ccsell == 1 || m->n_cols >= ((int64_t)1 << 23);
+}
+
+sm_status upload_ccsell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    const int32_t cl = m->opts.ccsell_chunk_log2 > 0 ? m->opts.ccsell_chunk_log2 : kCcDefaultChunkLog2;
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    const bool cb = m->opts.sell_codebook != 0 && cl <= 24 && codebook_ids(val, m->nnz, table, ids);
+    if (!cb) std::vector<uint8_t>().swap(ids);
+    CcsellHost h;
+    // SM_CCSELL_ROWORDER (development A/B): units in row order instead of by length.
+    const char *ro = dev_env("SM_CCSELL_ROWORDER");
+    const bool by_length = !(ro && atoi(ro) == 1);
+    if (!ccsell_build(rp, col, val, cb ? ids.data() : nullptr, m->n_rows, m->n_cols, cl, h, by_length))
+        return SM_OK;   // not applicable: the sliced ELL serves the matrix
+    std::vector<uint8_t>().swap(ids);
+    if (h.n_slices == 0) return SM_OK;
+    CcsellDev &d = m->plan.cc;
+    SM_TRY_HIP(dev_alloc(&d.d_off, h.n_slices, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_len, h.n_slices, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_row, h.n_slices * kSellLanes, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_row_len, h.n_slices * kSellLanes, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(h.padded, 1), m->device_bytes));
+    if (cb) {
+        SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
+        if (!table.empty())
+            SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+        d.table_size = (int32_t)table.size();
+    } else {
+        SM_TRY_HIP(dev_alloc(&d.d_val, std::max<int64_t>(h.padded, 1), m->device_bytes));
+        if (h.padded)
+            SM_TRY_HIP(hipMemcpy(d.d_val, h.val.data(), (size_t)h.padded * 4, hipMemcpyHostToDevice));
+    }
+    SM_TRY_HIP(hipMemcpy(d.d_off, h.off.data(), h.off.size() * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_len, h.len.data(), h.len.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_row, h.row.data(), h.row.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_row_len, h.row_len.data(), h.row_len.size() * 2, hipMemcpyHostToDevice));
+    if (h.padded)
+        SM_TRY_HIP(hipMemcpy(d.d_word, h.word.data(), (size_t)h.padded * 4, hipMemcpyHostToDevice));
+    d.n_chunks = h.n_chunks;
+    d.chunk_log2 = h.chunk_log2;
+    d.chunk_slice = std::move(h.chunk_slice);
+    d.n_slices = h.n_slices;
     return SM_OK;
 }
 
@@ -604,6 +675,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     sm_status st2 = upload_plan(m, rp);
     if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting(m));
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
+    if (st2 == SM_OK && want_ccsell(m)) st2 = upload_ccsell(m, rp, col, val);
     if (st2 == SM_OK && want_sell(m)) st2 = upload_sell(m, rp, col, val);
     return st2;
 }
@@ -813,6 +885,7 @@ void sm_build_opts_init(sm_build_opts *o) {
     o->sell = -1;
     o->sell_codebook = -1;
     o->relabel = -1;
+    o->ccsell = -1;
 }
 
 sm_status sm_create_from_csr(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t *row_ptr,
@@ -943,6 +1016,8 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
         if (st == SM_OK && xband) st = values();
         if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting(m.get()));
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
+        if (st == SM_OK && want_ccsell(m.get())) st = values();
+        if (st == SM_OK && want_ccsell(m.get())) st = upload_ccsell(m.get(), rp.data(), ch.data(), vh.data());
         if (st == SM_OK && want_sell(m.get())) st = values();
         if (st == SM_OK && want_sell(m.get())) st = upload_sell(m.get(), rp.data(), ch.data(), vh.data());
     }
@@ -986,7 +1061,8 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;
-    info->sell_codebook = m->plan.sell.d_table != nullptr;
+    info->sell_codebook = m->plan.sell.d_table != nullptr || m->plan.cc.d_table != nullptr;
+    info->ccsell_chunks = m->plan.cc.n_slices > 0 ? m->plan.cc.n_chunks : 0;
     // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
     memcpy(out, &full, std::min(info_bytes, sizeof(full)));
     return SM_OK;
@@ -1117,6 +1193,10 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         // fall through: no band layout (or unaligned x) -> sell or stream kernel
         [[fallthrough]];
     case SM_ALGO_SELL:
+        if (m->plan.cc.n_slices > 0) {   // column-chunked: no scratch, y read and written per chunk
+            e = launch_spmv_ccsell(m->plan.cc, x, y, alpha, beta, s);
+            break;
+        }
         if (m->plan.sell.n_slices > 0) {
             const float *xs = x;
             if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns

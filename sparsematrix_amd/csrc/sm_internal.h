@@ -49,6 +49,8 @@ struct BuildOpts {
     int64_t sell_sigma = 0;
     int32_t relabel = -1;
     int32_t tile_nnz = 0;
+    int32_t ccsell = -1;
+    int32_t ccsell_chunk_log2 = 0;
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
@@ -104,9 +106,25 @@ struct SellDev {
     float *d_partials = nullptr;      // one per segment (one SpMV in flight per matrix)
 };
 
+// Device copy of the column-chunked sorted sliced-ELL layout (ccsell.h).
+struct CcsellDev {
+    int64_t n_slices = 0;             // 0 when not built
+    int32_t n_chunks = 0, chunk_log2 = 0;
+    std::vector<int64_t> chunk_slice; // host: n_chunks + 1 (one launch per chunk)
+    int64_t *d_off = nullptr;
+    int32_t *d_len = nullptr;
+    int32_t *d_row = nullptr;         // row | kCcFirst, -1: no row
+    uint16_t *d_row_len = nullptr;
+    uint32_t *d_word = nullptr;       // column in chunk (| id << chunk_log2 in the codebook form)
+    float *d_val = nullptr;           // plain form
+    float *d_table = nullptr;         // codebook form
+    int32_t table_size = 0;
+};
+
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
+    CcsellDev cc;                     // n_slices == 0 when not built
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -141,6 +159,9 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
 // y[long_rows[i]] = beta * y + partials[long_ptr[i] .. long_ptr[i+1]) in order.
 hipError_t launch_long_finalize(int32_t n_long, const int32_t *long_rows, const int32_t *long_ptr,
                                 const float *partials, float *y, float beta, hipStream_t s);
+// Column-chunked sorted sliced-ELL (kernels_ccsell.hip): one launch per column chunk.
+hipError_t launch_spmv_ccsell(const CcsellDev &cd, const float *x, float *y, float alpha,
+                              float beta, hipStream_t s);
 // Balanced-band kind (kernels_band2.hip).
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);

@@ -55,3 +55,19 @@ def test_sell_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sell_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_ccsell_builder_under_asan(tmp_path):
+    """Column-chunked sliced-ELL builder (ccsell.cpp): walking chunks in order, every row's
+    terms once in ascending column order, one first-flagged unit per row, sorted slices."""
+    exe = tmp_path / "ccsell_asan"
+    src = [os.path.join(ROOT, "tests", "native", "ccsell_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "ccsell.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ccsell_asan: ok" in r.stdout
