@@ -76,9 +76,13 @@ typedef enum sm_algo {
     SM_ALGO_XBAND = 4,    /* x staged through LDS in column bands (the layout built at
                              creation, see sm_info.has_xband); falls back to SELL, then
                              STREAM, when the matrix holds no band layout             */
-    SM_ALGO_SELL = 5      /* sorted sliced-ELL, one lane per row (every row up to 2048
+    SM_ALGO_SELL = 5,     /* sorted sliced-ELL, one lane per row (every row up to 2048
                              terms bit-identical; longer rows in 2048-term segments whose
                              sums are added in order); STREAM when not built           */
+    SM_ALGO_NATIVE = 6    /* the reference's own stream (uint8 deltas + ids, 256-column
+                             panels) decoded on the device; bit-identical for every
+                             output; only for matrices built from the dense index
+                             (SM_ERR_NOT_SUPPORTED otherwise)                          */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the
@@ -116,6 +120,9 @@ typedef struct sm_info {
     int32_t sell_codebook;      /* 1: the slices hold 4-byte column | codebook-id words */
     int32_t ccsell_chunks;      /* column chunks of the column-chunked sliced ELL (0: not built);
                                    it serves SpMV when built (AUTO, SELL): every row bit-identical */
+    int32_t hot_cols;           /* > 0: the relabeled columns [0, hot_cols) run as codebook bands
+                                   before the sliced ELL adds the other terms (AUTO, SELL)  */
+    int32_t reserved1;
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -198,6 +205,10 @@ typedef struct sm_build_opts {
     int32_t ccsell;            /* column-chunked sliced-ELL (wide x): -1 auto, 0 never, 1 always
                                   (where no band layout is built and it applies)       */
     int32_t ccsell_chunk_log2; /* its column chunk, log2 columns (8..24), 0 = 20 (4 MiB of x) */
+    int32_t hot_cols;          /* skewed graphs (column relabeling built): the hottest this many
+                                  relabeled columns go through codebook bands with x in LDS,
+                                  the rest through the sliced ELL; 0 auto, -1 never        */
+    int32_t reserved_opts;
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);

@@ -31,7 +31,7 @@ SM_ERR_NO_DEVICE = 7
 
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
-ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5}
+ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5, "native": 6}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
@@ -64,6 +64,7 @@ class SmInfo(C.Structure):
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
         ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("ccsell_chunks", C.c_int32),
+        ("hot_cols", C.c_int32), ("reserved1", C.c_int32),
     ]
 
 
@@ -78,7 +79,8 @@ class SmBuildOpts(C.Structure):
         ("band_tall", C.c_int32), ("gather_band_log2", C.c_int32), ("sell", C.c_int32),
         ("sell_codebook", C.c_int32), ("sell_max_len", C.c_int32), ("sell_streams", C.c_int32),
         ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
-        ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32),
+        ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32), ("hot_cols", C.c_int32),
+        ("reserved_opts", C.c_int32),
     ]
 
 

@@ -71,6 +71,17 @@ hipError_t dev_alloc(T **p, int64_t count, int64_t &acct) {
     return e;
 }
 
+void free_xband_dev(XbandDev &h) {
+    (void)hipFree(h.d_chunk_start);
+    (void)hipFree(h.d_word);
+    (void)hipFree(h.d_val);
+    (void)hipFree(h.d_partials);
+    (void)hipFree(h.d_tickets);
+    (void)hipFree(h.d_band_clo);
+    (void)hipFree(h.d_table);
+    h = XbandDev();
+}
+
 void free_device(sm_matrix *m) {
     DeviceGuard g(m->device);
     (void)hipFree(m->d_row_ptr);
@@ -108,6 +119,13 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.cc.d_word);
     (void)hipFree(m->plan.cc.d_val);
     (void)hipFree(m->plan.cc.d_table);
+    (void)hipFree(m->plan.nat.d_pos);
+    (void)hipFree(m->plan.nat.d_val);
+    (void)hipFree(m->plan.nat.d_beg);
+    (void)hipFree(m->plan.nat.d_end);
+    (void)hipFree(m->plan.nat.d_col);
+    (void)hipFree(m->plan.nat.d_table);
+    free_xband_dev(m->plan.hot);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
     if (m->scratch_ready) (void)hipEventDestroy(m->scratch_ready);
@@ -160,6 +178,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.tile_nnz = d.tile_nnz;
         r.ccsell = d.ccsell;
         r.ccsell_chunk_log2 = d.ccsell_chunk_log2;
+        r.hot_cols = d.hot_cols;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -179,6 +198,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     if (const char *e = dev_env("SM_TILE_NNZ")) r.tile_nnz = atoi(e);
     if (const char *e = dev_env("SM_CCSELL")) r.ccsell = atoi(e);
     if (const char *e = dev_env("SM_CCSELL_CHUNK")) r.ccsell_chunk_log2 = atoi(e);
+    if (const char *e = dev_env("SM_HOT_COLS")) r.hot_cols = atoi(e);
     return r;
 }
 
@@ -200,6 +220,7 @@ sm_status check_opts(const sm_build_opts *o) {
         return fail(SM_ERR_INVALID_ARG, "negative sell option");
     if (r.ccsell_chunk_log2 != 0 && (r.ccsell_chunk_log2 < 8 || r.ccsell_chunk_log2 > 24))
         return fail(SM_ERR_INVALID_ARG, "ccsell_chunk_log2 must be 0 or 8..24");
+    if (r.hot_cols < -1) return fail(SM_ERR_INVALID_ARG, "hot_cols must be -1, 0 or positive");
     return SM_OK;
 }
 
@@ -263,32 +284,32 @@ bool want_xband(const sm_matrix *m) {
 // Balanced-band layout (band2.cpp, kernels_band2.hip): slabs so there are about
 // kXbTargetTiles tiles of <= 16K rows.  kind cband: 4-byte codebook words when the
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
-static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
-                              const float *val, XbKind kind) {
-    // Geometry: band_tall = 1 takes the tall tiles (xband.h B2Geom).
-    const bool tall = m->opts.band_tall == 1;
+// Builds into `d` the balanced bands of an n_rows x n_cols CSR (the matrix's own, or
+// the hot column prefix of a relabeled graph); `forced`: keep mostly-padding bands.
+static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                             const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
+                             bool tall, int32_t slabs, bool forced) {
     const B2Geom geom = !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
-    const int64_t br = std::min<int64_t>(geom.block_rows, m->n_rows);
-    const int64_t nblk = (m->n_rows + br - 1) / br;
+    const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
+    const int64_t nblk = (n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
         1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
-    if (m->opts.band_slabs > 0) want = std::max(1, std::min(16, m->opts.band_slabs));
+    if (slabs > 0) want = std::max(1, std::min(16, slabs));
     std::vector<float> table;
     std::vector<uint8_t> ids;
-    const bool cb = kind == kXbCband && codebook_ids(val, m->nnz, table, ids);
+    const bool cb = kind == kXbCband && codebook_ids(val, nnz, table, ids);
     Band2Host bh;
     const B2Geom g = !tall ? kB2Wide : cb ? kB2TallCb : kB2TallB2;
-    if (!band2_build(rp, col, val, m->n_rows, m->n_cols, want, bh, cb ? ids.data() : nullptr, g))
+    if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, g))
         return SM_OK;
     std::vector<uint8_t>().swap(ids);
     // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
     // dummies (wide or very sparse matrices), the padding would cost more HBM bytes
     // than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
-    if (!kind_forced(m) && bh.n_bands > 0 &&
+    if (!forced && bh.n_bands > 0 &&
         (double)bh.real_terms < 0.7 * (double)bh.n_bands * kB2Chunks * 64)
         return SM_OK;
     const int64_t band_words = cb ? 2048 : 4096;
-    XbandDev &d = m->plan.xb;
     const int64_t ntile = (int64_t)bh.n_blocks * bh.n_slabs;
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, bh.n_bands), m->device_bytes));
@@ -301,7 +322,7 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
         d.table_size = (int32_t)table.size();
     }
     if (bh.n_slabs > 1) {
-        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
+        const int64_t ps = (n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(bh.n_slabs - 1) * ps, m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)bh.n_blocks, m->device_bytes));
         SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)bh.n_blocks * 4 * sizeof(int32_t)));
@@ -325,6 +346,13 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
     return SM_OK;
+}
+
+static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
+                              const float *val, XbKind kind) {
+    // Geometry: band_tall = 1 takes the tall tiles (xband.h B2Geom).
+    return build_band2(m, m->plan.xb, m->n_rows, m->n_cols, m->nnz, rp, col, val, kind,
+                       m->opts.band_tall == 1, m->opts.band_slabs, kind_forced(m));
 }
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
@@ -468,11 +496,13 @@ bool want_sell(const sm_matrix *m) {
     return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0 && m->plan.cc.n_slices == 0;
 }
 
-sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
+                      int64_t nnz = -1, bool cols_relabeled = false) {
     Plan &p = m->plan;
+    if (nnz < 0) nnz = m->nnz;
     std::vector<int32_t> rcol;
     const int32_t *c = col;
-    if (p.n_relabel > 0) {   // the layout stores relabeled columns (x is permuted per SpMV)
+    if (p.n_relabel > 0 && !cols_relabeled) {   // the layout stores relabeled columns (x is permuted per SpMV)
         rcol.resize((size_t)m->nnz);
         SM_TRY_HIP(hipMemcpy(rcol.data(), p.d_rcol, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
         c = rcol.data();
@@ -489,7 +519,7 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     std::vector<float> table;
     std::vector<uint8_t> ids;
     const bool cb = m->opts.sell_codebook != 0 && m->n_cols <= ((int64_t)1 << kSellCbColBits) &&
-                    codebook_ids(val, m->nnz, table, ids);
+                    codebook_ids(val, nnz, table, ids);
     if (!cb) std::vector<uint8_t>().swap(ids);
     SellHost sh;
     sell_build(rp, c, val, m->n_rows, max_len, sh, sigma, streams, cb ? ids.data() : nullptr);
@@ -594,6 +624,107 @@ sm_status upload_ccsell(sm_matrix *m, const int32_t *rp, const int32_t *col, con
     return SM_OK;
 }
 
+// The reference's stream on the device (native.hip, SM_ALGO_NATIVE): each panel's run
+// padded to start at a multiple of 16 bytes with (delta 0, id T) fillers, which the
+// decode skips like the reference's own fillers -- so every 16-entry load is aligned.
+sm_status upload_native(sm_matrix *m) {
+    if (!m->has_ref || m->panel_col_off.empty() || m->table_size <= 0) return SM_OK;
+    if (m->s_rows >= ((int64_t)1 << 23)) return SM_OK;   // in-panel offsets in int32
+    const size_t P = m->panel_col_off.size();
+    std::vector<uint8_t> pos, val;
+    std::vector<int64_t> beg(P), end(P);
+    pos.reserve(m->pos.size() + 16 * P);
+    val.reserve(m->pos.size() + 16 * P);
+    for (size_t p = 0; p < P; p++) {
+        while (pos.size() % 16) { pos.push_back(0); val.push_back((uint8_t)m->table_size); }
+        beg[p] = (int64_t)pos.size();
+        pos.insert(pos.end(), m->pos.begin() + m->panel_begin[p], m->pos.begin() + m->panel_end[p]);
+        val.insert(val.end(), m->val.begin() + m->panel_begin[p], m->val.begin() + m->panel_end[p]);
+        end[p] = (int64_t)pos.size();
+    }
+    NativeDev &d = m->plan.nat;
+    SM_TRY_HIP(dev_alloc(&d.d_pos, (int64_t)pos.size() + 16, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_val, (int64_t)val.size() + 16, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_beg, (int64_t)P, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_end, (int64_t)P, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_col, (int64_t)P, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
+    SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
+    SM_TRY_HIP(hipMemcpy(d.d_pos, pos.data(), pos.size(), hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_val, val.data(), val.size(), hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_beg, beg.data(), P * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_end, end.data(), P * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_col, m->panel_col_off.data(), P * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_table, m->table.data(), (size_t)m->table_size * 4, hipMemcpyHostToDevice));
+    d.table_size = m->table_size;
+    d.s_rows = m->s_rows;
+    d.s_cols = m->s_cols;
+    d.n_panels = (int32_t)P;
+    return SM_OK;
+}
+
+// Skewed graphs (column relabeling built, e.g. R-MAT): the hottest
+// relabeled columns [0, H) hold a large share of the terms in few columns, so they go
+// through the codebook band kernel with their x staged in LDS (kernels_band2.hip) --
+// no gathers -- and the sliced ELL gathers only the rest.  A row then adds its hot
+// terms (in relabeled column order) before its cold ones (stored order): within the
+// Sum|terms| bound, deterministic.  AUTO takes H = 32768 when the hot prefix holds
+// >= 15 % of the terms and the graph has >= 2^18 rows; hot_cols = -1 never, > 0 forces H.
+constexpr int32_t kHotColsDefault = 32768;
+
+sm_status upload_sell_layouts(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    Plan &p = m->plan;
+    const int64_t H0 = m->opts.hot_cols < 0 ? 0 : m->opts.hot_cols > 0 ? m->opts.hot_cols : kHotColsDefault;
+    const bool try_hot = p.n_relabel > 0 && H0 > 0 && H0 < m->n_cols &&
+                         (m->opts.hot_cols > 0 || m->n_rows >= (1 << 18));
+    if (!try_hot) return upload_sell(m, rp, col, val);
+    const int64_t nnz = m->nnz, nr = m->n_rows;
+    std::vector<int32_t> rcol((size_t)nnz);
+    SM_TRY_HIP(hipMemcpy(rcol.data(), p.d_rcol, (size_t)nnz * 4, hipMemcpyDeviceToHost));
+    int64_t hot = 0;
+    for (int64_t e = 0; e < nnz; e++) hot += rcol[(size_t)e] < H0;
+    if (m->opts.hot_cols == 0 && (double)hot < 0.15 * (double)nnz)
+        return upload_sell(m, rp, rcol.data(), val, nnz, true);
+    // Split every row into its hot part (sorted by relabeled column: the bands need
+    // ascending columns) and its cold part (stored order).
+    std::vector<int32_t> rph((size_t)nr + 1, 0), rpc((size_t)nr + 1, 0);
+    std::vector<int32_t> ch((size_t)hot), cc((size_t)(nnz - hot));
+    std::vector<float> vh((size_t)hot), vc((size_t)(nnz - hot));
+    std::vector<std::pair<int32_t, float>> tmp;
+    int64_t oh = 0, oc = 0;
+    for (int64_t r = 0; r < nr; r++) {
+        tmp.clear();
+        for (int32_t e = rp[r]; e < rp[r + 1]; e++) {
+            if (rcol[(size_t)e] < H0) {
+                tmp.push_back({rcol[(size_t)e], val[e]});
+            } else {
+                cc[(size_t)oc] = rcol[(size_t)e];
+                vc[(size_t)oc++] = val[e];
+            }
+        }
+        std::sort(tmp.begin(), tmp.end(),
+                  [](const std::pair<int32_t, float> &a, const std::pair<int32_t, float> &b) { return a.first < b.first; });
+        for (const auto &t : tmp) {
+            ch[(size_t)oh] = t.first;
+            vh[(size_t)oh++] = t.second;
+        }
+        rph[(size_t)r + 1] = (int32_t)oh;
+        rpc[(size_t)r + 1] = (int32_t)oc;
+    }
+    std::vector<int32_t>().swap(rcol);
+    sm_status st = build_band2(m, p.hot, nr, H0, hot, rph.data(), ch.data(), vh.data(), kXbCband,
+                               false, 0, true);
+    if (st != SM_OK) return st;
+    if (p.hot.n_blocks == 0 || p.hot.kind != kXbCband) {   // not applicable: sell serves all terms
+        free_xband_dev(p.hot);
+        return upload_sell(m, rp, col, val);
+    }
+    p.hot_cols = (int32_t)H0;
+    std::vector<int32_t>().swap(ch);
+    std::vector<float>().swap(vh);
+    return upload_sell(m, rpc.data(), cc.data(), vc.data(), nnz - hot, true);
+}
+
 sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     PlanHost ph;
     int32_t tile = tile_nnz_setting(m);
@@ -676,7 +807,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting(m));
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     if (st2 == SM_OK && want_ccsell(m)) st2 = upload_ccsell(m, rp, col, val);
-    if (st2 == SM_OK && want_sell(m)) st2 = upload_sell(m, rp, col, val);
+    if (st2 == SM_OK && want_sell(m)) st2 = upload_sell_layouts(m, rp, col, val);
     return st2;
 }
 
@@ -777,6 +908,7 @@ sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t
     std::vector<int32_t> rp32(er.row_ptr.size());
     for (size_t i = 0; i < rp32.size(); i++) rp32[i] = (int32_t)er.row_ptr[i];
     st = finish_from_host_csr(m.get(), rp32.data(), er.col.data(), er.val.data());
+    if (st == SM_OK) st = upload_native(m.get());
     if (st != SM_OK) {
         free_device(m.get());
         return st;
@@ -1019,7 +1151,7 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
         if (st == SM_OK && want_ccsell(m.get())) st = values();
         if (st == SM_OK && want_ccsell(m.get())) st = upload_ccsell(m.get(), rp.data(), ch.data(), vh.data());
         if (st == SM_OK && want_sell(m.get())) st = values();
-        if (st == SM_OK && want_sell(m.get())) st = upload_sell(m.get(), rp.data(), ch.data(), vh.data());
+        if (st == SM_OK && want_sell(m.get())) st = upload_sell_layouts(m.get(), rp.data(), ch.data(), vh.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }
     *out = m.release();
@@ -1063,6 +1195,7 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->sell_slices = m->plan.sell.n_slices;
     info->sell_codebook = m->plan.sell.d_table != nullptr || m->plan.cc.d_table != nullptr;
     info->ccsell_chunks = m->plan.cc.n_slices > 0 ? m->plan.cc.n_chunks : 0;
+    info->hot_cols = m->plan.hot.n_blocks > 0 ? m->plan.hot_cols : 0;
     // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
     memcpy(out, &full, std::min(info_bytes, sizeof(full)));
     return SM_OK;
@@ -1155,12 +1288,22 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (beta != 1.0f) e = launch_beta(y, 1, n, n, beta, s);
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv beta");
     }
+    if (algo == SM_ALGO_NATIVE) {   // the reference stream: y = x * S (a = x, c = y, m = 1)
+        if (!m->has_ref || (m->plan.nat.n_panels == 0 && m->nnz > 0))
+            return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_NATIVE needs a matrix built from the dense index");
+        e = m->plan.nat.n_panels == 0 ? (beta != 1.0f ? launch_beta(y, 1, n, n, beta, s) : hipSuccess)
+                                      : launch_native_addmatmat(m->plan.nat, 1, x, (int32_t)m->n_cols, y,
+                                                                n, alpha, beta, s);
+        e = after_launch(e, s, "sm_spmv native");
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv native");
+    }
     if (algo < SM_ALGO_AUTO || algo > SM_ALGO_SELL) return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     // The matrix's SpMV scratch (sm_internal.h): SpMVs that use it run one after the
     // other on the device, whatever stream or thread issues them.
     const Plan &pl = m->plan;
     const bool scratch = algo != SM_ALGO_PARITY && algo != SM_ALGO_VECTOR &&
                          ((pl.xb.n_blocks > 0 && pl.xb.n_slabs > 1) || pl.n_relabel > 0 ||
+                          (pl.hot.n_blocks > 0 && pl.hot.n_slabs > 1) ||
                           pl.sell.n_long > 0 || pl.n_long > 0);
     std::unique_lock<std::mutex> lk(m->scratch_mu, std::defer_lock);
     bool ordered = false;
@@ -1203,7 +1346,12 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
                 e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
                 xs = m->plan.d_xperm;
             }
-            if (e == hipSuccess) e = launch_spmv_sell(m->plan.sell, xs, y, alpha, beta, s);
+            float b = beta;
+            if (e == hipSuccess && m->plan.hot.n_blocks > 0) {   // hot columns first, then the rest
+                e = launch_spmv_band2(m->plan.hot, n, m->plan.hot_cols, xs, y, alpha, beta, s);
+                b = 1.0f;
+            }
+            if (e == hipSuccess) e = launch_spmv_sell(m->plan.sell, xs, y, alpha, b, s);
             break;
         }
         [[fallthrough]];   // no sell layout -> stream kernel
@@ -1270,13 +1418,22 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
     if (m == 0 || n == 0) return SM_OK;
     if (ldc < n || (alpha != 0.0f && lda < k)) return fail(SM_ERR_INVALID_ARG, "lda/ldc too small");
     if (!c || (alpha != 0.0f && k > 0 && !a)) return fail(SM_ERR_INVALID_ARG, "null a/c");
-    if (m == 1) return sm_spmv(mat, alpha, a, beta, c, algo, stream);
+    if (m == 1 && algo != SM_ALGO_NATIVE) return sm_spmv(mat, alpha, a, beta, c, algo, stream);
     DeviceGuard g(mat->device);
     hipStream_t s = (hipStream_t)stream;
     hipError_t e;
     if (alpha == 0.0f) {
         e = beta != 1.0f ? launch_beta(c, m, (int32_t)n, ldc, beta, s) : hipSuccess;
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat beta");
+    }
+    if (algo == SM_ALGO_NATIVE) {   // the reference stream, A and C read in place
+        if (!mat->has_ref || (mat->plan.nat.n_panels == 0 && mat->nnz > 0))
+            return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_NATIVE needs a matrix built from the dense index");
+        e = mat->plan.nat.n_panels == 0
+                ? (beta != 1.0f ? launch_beta(c, m, (int32_t)n, ldc, beta, s) : hipSuccess)
+                : launch_native_addmatmat(mat->plan.nat, m, a, lda, c, ldc, alpha, beta, s);
+        e = after_launch(e, s, "sm_addmatmat native");
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat native");
     }
     if (algo != SM_ALGO_PARITY && m <= 128 && k > 0) {
         // C^T = B A^T through the row-panel SpMM (the reference transposes too,

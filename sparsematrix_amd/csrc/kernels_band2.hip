@@ -334,57 +334,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
 
-    if constexpr (CB) {
-        if constexpr (256 * kTabCopies < 4 * kB2Threads) {   // at most two entries per thread
-            for (int i = tid; i < 256 * kTabCopies; i += kB2Threads) {
-                const int id = i / kTabCopies;
-                tab[i] = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
-            }
-        } else {
-            constexpr int kPer = 256 * kTabCopies / kB2Threads;   // copies written per thread
-            static_assert(kPer % 4 == 0 && kTabCopies % kPer == 0, "whole float4 of one entry");
-            const int id = tid / (kTabCopies / kPer);   // one entry per thread
-            const float v = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
-#pragma unroll
-            for (int j = 0; j < kPer; j += 4)
-                *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
-        }
-    }
-    // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row
-    // without terms in this slab keeps the sign of a zero y), all loads in flight.
-    constexpr int kQ = BROWS / (4 * kB2Threads);
-    const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
-    if (slab == 0) {
-        const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
-        float4 v[kQ];
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            const uint32_t o = 16u * (uint32_t)(tid + q * kB2Threads);
-            if (y_vec) {
-                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(yi_src, o, 0, 0);
-                v[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
-                                   __uint_as_float(u.z), __uint_as_float(u.w));
-            } else {
-                v[q] = make_float4(
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o, 0, 0)),
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 4, 0, 0)),
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 8, 0, 0)),
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 12, 0, 0)));
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            if (beta != 1.0f)
-                v[q] = make_float4(__fmul_rn(v[q].x, beta), __fmul_rn(v[q].y, beta),
-                                   __fmul_rn(v[q].z, beta), __fmul_rn(v[q].w, beta));
-            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = v[q];
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < kQ; ++q)
-            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
-    }
-
+    // Prologue, ordered so its memory latencies overlap: the first windows' x and entry
+    // loads go out first, then the codebook and (slab 0) y loads; the LDS writes of all
+    // of them follow, so the tile waits about one memory latency before its first band
+    // instead of one per kind of load (vmcnt retires in issue order).
     // Rings with static roles: x window q in X[q % AX], entries of band q in E[q % AE].
     // Prologue = virtual bands -U..-1 (their loads in the loop's order), so the loads
     // pending at the loop header are in the order the loop's back edge leaves them.
@@ -401,8 +354,66 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if (v + AX >= 0) load_x(v + AX, X[v + AX]);
             if (v + AE >= 0) E[(v + AE) % ER] = load_e(v + AE);
         }
-        store_x(0, X[0]);
     }
+    // Codebook: fl(table[id] * alpha), loaded now, written below.
+    constexpr bool kTabSmall = 256 * kTabCopies < 4 * kB2Threads;   // at most two entries per thread
+    constexpr int kPer = kTabSmall ? 1 : 256 * kTabCopies / kB2Threads;   // copies written per thread
+    float tab_v = 0.0f;
+    if constexpr (CB && !kTabSmall) {
+        static_assert(kPer % 4 == 0 && kTabCopies % kPer == 0, "whole float4 of one entry");
+        const int id = tid / (kTabCopies / kPer);   // one entry per thread
+        tab_v = id < table_size ? table[id] : 0.0f;
+    }
+    // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row
+    // without terms in this slab keeps the sign of a zero y), all loads in flight.
+    constexpr int kQ = BROWS / (4 * kB2Threads);
+    const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
+    float4 yv[kQ];
+    if (slab == 0) {
+        const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const uint32_t o = 16u * (uint32_t)(tid + q * kB2Threads);
+            if (y_vec) {
+                const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(yi_src, o, 0, 0);
+                yv[q] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                    __uint_as_float(u.z), __uint_as_float(u.w));
+            } else {
+                yv[q] = make_float4(
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 4, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 8, 0, 0)),
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(yi_src, o + 12, 0, 0)));
+            }
+        }
+    }
+    if constexpr (CB) {
+        if constexpr (kTabSmall) {
+            for (int i = tid; i < 256 * kTabCopies; i += kB2Threads) {
+                const int id = i / kTabCopies;
+                tab[i] = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
+            }
+        } else {
+            const float v = __fmul_rn(tab_v, alpha);
+#pragma unroll
+            for (int j = 0; j < kPer; j += 4)
+                *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
+        }
+    }
+    if (slab == 0) {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            if (beta != 1.0f)
+                yv[q] = make_float4(__fmul_rn(yv[q].x, beta), __fmul_rn(yv[q].y, beta),
+                                    __fmul_rn(yv[q].z, beta), __fmul_rn(yv[q].w, beta));
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = yv[q];
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
+    }
+    if constexpr (!kDma) store_x(0, X[0]);
     __syncthreads();
 
     // Whole groups of U bands (static ring indices, no branch around a load or a

@@ -51,6 +51,7 @@ struct BuildOpts {
     int32_t tile_nnz = 0;
     int32_t ccsell = -1;
     int32_t ccsell_chunk_log2 = 0;
+    int32_t hot_cols = 0;
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
@@ -121,10 +122,27 @@ struct CcsellDev {
     int32_t table_size = 0;
 };
 
+// Device copy of the reference's own stream (native.hip): uint8 deltas + ids, each
+// panel's run starting 16-byte aligned (padded with zero-delta fillers).
+struct NativeDev {
+    int32_t n_panels = 0;             // 0 when not built
+    int64_t s_rows = 0, s_cols = 0;
+    uint8_t *d_pos = nullptr, *d_val = nullptr;
+    int64_t *d_beg = nullptr, *d_end = nullptr;
+    int32_t *d_col = nullptr;
+    float *d_table = nullptr;         // table_size raw values
+    int32_t table_size = 0;
+};
+
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
     CcsellDev cc;                     // n_slices == 0 when not built
+    NativeDev nat;                    // n_panels == 0 when not built (dense-index matrices)
+    // Skewed graphs: the hottest relabeled columns [0, hot_cols) as codebook bands (x in
+    // LDS), the sell layout holding only the other terms.
+    XbandDev hot;                     // n_blocks == 0 when not built
+    int32_t hot_cols = 0;
     int32_t tile_nnz = kTileNnz;      // one of 1024, 2048, 4096, 8192
     int32_t n_tiles = 0;
     Tile *d_tiles = nullptr;
@@ -162,6 +180,9 @@ hipError_t launch_long_finalize(int32_t n_long, const int32_t *long_rows, const 
 // Column-chunked sorted sliced-ELL (kernels_ccsell.hip): one launch per column chunk.
 hipError_t launch_spmv_ccsell(const CcsellDev &cd, const float *x, float *y, float alpha,
                               float beta, hipStream_t s);
+// AddMatMat on the reference's stream (native.hip): C = alpha * A * S + beta * C.
+hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *a, int32_t lda,
+                                   float *c, int32_t ldc, float alpha, float beta, hipStream_t s);
 // Balanced-band kind (kernels_band2.hip).
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);

@@ -784,3 +784,67 @@ def test_golden_spmv_cband_and_sell(sm, name):
             y = to_dev(Cin[0].copy())
             M.spmv(to_dev(A[0].copy()), y, r.alpha, r.beta, algo="auto")
             assert bits_equal(to_host(y), want[0]), (lay, r.alpha, r.beta)
+
+
+def test_config3_spmm_full_size_vs_oracle(sm):
+    """BASELINE config 3 at full size, as bench.py runs it: the config-2 matrix (2^20 x 2^20,
+    16 distinct columns per row, seed 2) times a 2^20 x 32 row-major X (seed 3), alpha 1,
+    beta 0.5, AUTO = spmm_rowpanel2: every output bit-identical to the reference order."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n, N = 1 << 20, 32
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.rand((n, N), generator=g, device="cuda") * 2 - 1
+    Y0 = torch.rand((n, N), generator=g, device="cuda") * 2 - 1
+    Y = Y0.clone()
+    M.spmm(X, Y, 1.0, 0.5)
+    got = to_host(Y)
+    want = oracle.csr_spmm(rp.cpu().numpy().astype(np.int64), ci.cpu().numpy(), va.cpu().numpy(),
+                           to_host(X), to_host(Y0), 1.0, 0.5)
+    assert bits_equal(got, want)
+
+
+# ------------------------------------------------------------- native-format kernel
+@pytest.mark.parametrize("name", case_names())
+def test_golden_addmatmat_native(sm, name):
+    """AddMatMat straight from the reference's uint8 delta/id stream on the device
+    (SM_ALGO_NATIVE, native.hip): bit-identical to the compiled reference's outputs
+    (every m, alpha, beta of the fixture, NaN in C included), and m = 1 through sm_spmv."""
+    c = load_case(name)
+    M = _from_case(sm, c)
+    k, n = c.s_rows, c.s_cols
+    for r in c.runs:
+        a_d, c_d = to_dev(r.a), to_dev(r.c)
+        M.AddMatMat(a_d, r.m, r.lda, c_d, r.ldc, r.alpha, r.beta, algo="native")
+        assert bits_equal(to_host(c_d), r.out), (r.m, r.alpha, r.beta)
+        A = r.a.reshape(r.m, r.lda)[:, :k]
+        Cin = r.c.reshape(r.m, r.ldc)[:, :n]
+        y = to_dev(Cin[0].copy())
+        M.spmv(to_dev(A[0].copy()), y, r.alpha, r.beta, algo="native")
+        assert bits_equal(to_host(y), r.out.reshape(r.m, r.ldc)[0, :n])
+
+
+@pytest.mark.parametrize("n,dens,m", [(16384, 0.001, 1), (4096, 0.25, 1), (2000, 0.05, 13),
+                                      (3000, 0.6, 32)])
+def test_native_vs_oracle_larger(sm, n, dens, m):
+    """Larger reference streams (fillers at 0.1 % density, dense panels at 25-60 %, long
+    panels spanning many 4096-entry chunks): the native kernel equals the restated
+    reference AddMatMat (oracle.RefModel) bit for bit; a CSR-built matrix refuses it."""
+    rng = np.random.default_rng(n + m)
+    table = rng.uniform(-1, 1, 200).astype(np.float32)
+    dm = np.where(rng.random((n, n)) < dens, rng.integers(0, 200, (n, n)), 255).astype(np.uint8)
+    M = sm.SparseMatrix(dm, n, n, n, table, 200, sm.SblasTrans)
+    ref = oracle.RefModel(dm, n, n, n, table, 200, trans=True)
+    A = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    C = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    for alpha, beta in ((1.0, 1.0), (1.3, 0.7), (-0.5, 0.0)):
+        want = ref.add_mat_mat(A.reshape(-1), m, n, C.reshape(-1), n, alpha, beta)
+        c_d = to_dev(C.reshape(-1))
+        M.AddMatMat(to_dev(A.reshape(-1)), m, n, c_d, n, alpha, beta, algo="native")
+        assert bits_equal(to_host(c_d), want), (alpha, beta)
+    rp, ci, va = M.csr()
+    Mc = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    with pytest.raises(sm.SparseMatrixError):
+        Mc.AddMatMat(to_dev(A.reshape(-1)), m, n, to_dev(C.reshape(-1)), n, 1.0, 1.0, algo="native")

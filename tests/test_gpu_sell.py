@@ -152,17 +152,93 @@ def test_sell_special_values(sm):
 
 
 def test_sell_rmat_auto(sm):
-    """AUTO without band layouts on an R-MAT graph (scale 20): column relabeling +
-    sell; short rows bit-exact, long rows within the bound."""
+    """R-MAT scale 20 without band layouts: column relabeling + codebook sell.  With the
+    hot-column bands off (hot_cols = -1) rows of up to 2048 terms are bit-exact; AUTO
+    (the hottest relabeled columns as codebook bands first, then the sliced ELL) stays
+    within 1e-6 * sum|terms| on every row."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     rp_d, ci_d, va_d = synth.rmat_device(20, 16, seed=4)
     n = 1 << 20
-    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands"))
+    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands", hot_cols=-1))
     info = M.info()
     assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
+    assert info["hot_cols"] == 0, info
     rp, ci, va = rp_d.cpu().numpy(), ci_d.cpu().numpy(), va_d.cpu().numpy()
     rng = np.random.default_rng(9)
     x = rng.uniform(-1, 1, n).astype(np.float32)
     y0 = rng.uniform(-1, 1, n).astype(np.float32)
     _check(M, rp, ci, va, x, y0, 1.0, 0.5, exact_max=2048)
+    H = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands"))
+    hinfo = H.info()
+    assert hinfo["hot_cols"] == 32768 and hinfo["col_relabel"] == 1, hinfo
+    for alpha, beta in ((1.0, 0.5), (1.3, 0.0), (-0.7, 1.0)):
+        _check(H, rp, ci, va, x, y0, alpha, beta, exact_max=0)
+        _check(H, rp, ci, va, x, y0, alpha, beta, algo="sell", exact_max=0)
+
+
+@pytest.mark.parametrize("hot", [8192, 40000])
+def test_hot_bands_forced_skewed(sm, hot):
+    """Forced hot-column split on a power-law-column matrix (relabeled): hot terms through
+    the codebook bands (one or several windows), the rest through the sliced ELL with its
+    long-row segments; special values and beta = 0 with NaN in y."""
+    rng = np.random.default_rng(hot)
+    n_rows, n_cols, per = 300000, 1 << 20, 12
+    label = rng.permutation(n_cols).astype(np.int32)
+    raw = np.minimum(rng.zipf(1.2, (n_rows, per)) - 1, n_cols - 1)
+    cols = np.sort(label[raw], axis=1)
+    keep = np.ones_like(cols, bool)
+    keep[:, 1:] = cols[:, 1:] != cols[:, :-1]
+    keep[7] = False                      # an empty row
+    lens = keep.sum(axis=1)
+    ci = cols[keep].astype(np.int32)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    table = rng.uniform(-1, 1, 255).astype(np.float32)
+    table[:3] = [np.inf, -0.0, 0.0]
+    va = table[rng.integers(0, 255, ci.size)]
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout="no_bands", relabel=1, hot_cols=hot))
+    info = M.info()
+    assert info["hot_cols"] == hot and info["sell_slices"] > 0, info
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    y0[::101] = np.nan
+    for alpha, beta in ((1.0, 1.0), (0.5, 0.0), (2.0, 3.0)):
+        _check(M, rp, ci, va, x, y0, alpha, beta, exact_max=0)
+
+
+def test_config4_rmat24_auto_vs_oracle(sm):
+    """BASELINE config 4 at full size, exactly as bench.py builds it: Graph500 R-MAT
+    scale 24, edgefactor 16, seed 4 (263 M terms, rows up to 238 465 terms), AUTO =
+    column relabeling + codebook sliced ELL with 2048-term segments.  Every row of up to
+    2048 terms is bit-identical to the reference order (oracle), the longer rows (their
+    segment sums added in order) within 1e-6 * sum|terms|."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    rp_d, ci_d, va_d = synth.rmat_device(24, 16, seed=4)
+    n = 1 << 24
+    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n)
+    info = M.info()
+    assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
+    assert info["max_row_nnz"] > 2048 and info["hot_cols"] > 0, info
+    E = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(hot_cols=-1))
+    assert E.info()["hot_cols"] == 0
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y, ye = y0.clone(), y0.clone()
+    M.spmv(x, y, 1.0, 0.5)
+    E.spmv(x, ye, 1.0, 0.5)
+    got, got_e = to_host(y), to_host(ye)
+    del M, E
+    rp, ci, va = rp_d.cpu().numpy(), ci_d.cpu().numpy(), va_d.cpu().numpy()
+    del rp_d, ci_d, va_d
+    xh, y0h = to_host(x), to_host(y0)
+    want = oracle.csr_spmv_mt(rp, ci, va, xh, y0h, 1.0, 0.5, threads=16)
+    lens = np.diff(rp.astype(np.int64))
+    short = lens <= 2048
+    # without the hot bands: every row of <= 2048 terms in the reference's order
+    assert np.array_equal(bits(got_e[short]), bits(want[short]))
+    # AUTO (hot bands, then the sliced ELL), and the long rows: the Sum|terms| bound
+    _, absum = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, xh, y0h, 1.0, 0.5)
+    assert_terms_close(got, want, absum)
+    assert_terms_close(got_e, want, absum)
