@@ -394,7 +394,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 tab[i] = id < table_size ? __fmul_rn(table[id], alpha) : 0.0f;
             }
         } else {
-            const float v = __fmul_rn(tab_v, alpha);
+            const int id = tid / (kTabCopies / kPer);
+            const float v = id < table_size ? __fmul_rn(tab_v, alpha) : 0.0f;
 #pragma unroll
             for (int j = 0; j < kPer; j += 4)
                 *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
