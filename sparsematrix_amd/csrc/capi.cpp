@@ -631,8 +631,21 @@ sm_status upload_native(sm_matrix *m) {
     if (!m->has_ref || m->panel_col_off.empty() || m->table_size <= 0) return SM_OK;
     if (m->s_rows >= ((int64_t)1 << 23)) return SM_OK;   // in-panel offsets in int32
     const size_t P = m->panel_col_off.size();
+    const size_t P_all = (size_t)((m->s_cols + 255) / 256);
     std::vector<uint8_t> pos, val;
-    std::vector<int64_t> beg(P), end(P);
+    // Panels with entries first, then every 256-column block without one (an empty run):
+    // a beta != 1 launch covers them all, since the kernel applies beta to the columns
+    // it owns and the reference scales all of C (sparse-matrix.cc:149-151).
+    std::vector<int64_t> beg(P, 0), end(P, 0);
+    std::vector<int32_t> cols(m->panel_col_off.begin(), m->panel_col_off.end());
+    {
+        std::vector<char> has(P_all, 0);
+        for (size_t p = 0; p < P; p++) has[(size_t)m->panel_col_off[p] / 256] = 1;
+        for (size_t q = 0; q < P_all; q++)
+            if (!has[q]) cols.push_back((int32_t)(q * 256));
+        beg.resize(cols.size(), 0);
+        end.resize(cols.size(), 0);
+    }
     pos.reserve(m->pos.size() + 16 * P);
     val.reserve(m->pos.size() + 16 * P);
     for (size_t p = 0; p < P; p++) {
@@ -645,21 +658,23 @@ sm_status upload_native(sm_matrix *m) {
     NativeDev &d = m->plan.nat;
     SM_TRY_HIP(dev_alloc(&d.d_pos, (int64_t)pos.size() + 16, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_val, (int64_t)val.size() + 16, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_beg, (int64_t)P, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_end, (int64_t)P, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_col, (int64_t)P, m->device_bytes));
+    const size_t Pc = cols.size();
+    SM_TRY_HIP(dev_alloc(&d.d_beg, (int64_t)Pc, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_end, (int64_t)Pc, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_col, (int64_t)Pc, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
     SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
     SM_TRY_HIP(hipMemcpy(d.d_pos, pos.data(), pos.size(), hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_val, val.data(), val.size(), hipMemcpyHostToDevice));
-    SM_TRY_HIP(hipMemcpy(d.d_beg, beg.data(), P * 8, hipMemcpyHostToDevice));
-    SM_TRY_HIP(hipMemcpy(d.d_end, end.data(), P * 8, hipMemcpyHostToDevice));
-    SM_TRY_HIP(hipMemcpy(d.d_col, m->panel_col_off.data(), P * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_beg, beg.data(), Pc * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_end, end.data(), Pc * 8, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_col, cols.data(), Pc * 4, hipMemcpyHostToDevice));
     SM_TRY_HIP(hipMemcpy(d.d_table, m->table.data(), (size_t)m->table_size * 4, hipMemcpyHostToDevice));
     d.table_size = m->table_size;
     d.s_rows = m->s_rows;
     d.s_cols = m->s_cols;
     d.n_panels = (int32_t)P;
+    d.n_all = (int32_t)Pc;
     return SM_OK;
 }
 

@@ -148,11 +148,12 @@ __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
 
 hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *a, int32_t lda,
                                    float *c, int32_t ldc, float alpha, float beta, hipStream_t s) {
-    if (nd.n_panels <= 0 || m <= 0) return hipSuccess;
+    const int32_t P = beta != 1.0f ? nd.n_all : nd.n_panels;   // empty blocks only scale
+    if (P <= 0 || m <= 0) return hipSuccess;
     if (!nd.d_pos || !nd.d_val || !nd.d_beg || !nd.d_end || !nd.d_col || !nd.d_table ||
         nd.table_size < 0 || nd.table_size > 255)
         return hipErrorInvalidValue;
-    const dim3 grid((unsigned)nd.n_panels, 256 / kNatCols, (unsigned)((m + kNatRows - 1) / kNatRows));
+    const dim3 grid((unsigned)P, 256 / kNatCols, (unsigned)((m + kNatRows - 1) / kNatRows));
     hipLaunchKernelGGL(native_addmatmat_kernel, grid, dim3(kNatThreads), 0, s, nd.d_pos, nd.d_val,
                        nd.d_beg, nd.d_end, nd.d_col, nd.d_table, nd.table_size,
                        (int32_t)nd.s_cols, m, a, lda, c, ldc, alpha, beta);

@@ -125,7 +125,8 @@ struct CcsellDev {
 // Device copy of the reference's own stream (native.hip): uint8 deltas + ids, each
 // panel's run starting 16-byte aligned (padded with zero-delta fillers).
 struct NativeDev {
-    int32_t n_panels = 0;             // 0 when not built
+    int32_t n_panels = 0;             // panels with entries; 0 when not built
+    int32_t n_all = 0;                // + the empty 256-column blocks (beta != 1 launches)
     int64_t s_rows = 0, s_cols = 0;
     uint8_t *d_pos = nullptr, *d_val = nullptr;
     int64_t *d_beg = nullptr, *d_end = nullptr;

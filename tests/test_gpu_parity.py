@@ -826,6 +826,27 @@ def test_golden_addmatmat_native(sm, name):
         assert bits_equal(to_host(y), r.out.reshape(r.m, r.ldc)[0, :n])
 
 
+def test_native_beta_scales_columns_without_panels(sm):
+    """Column blocks with no entries have no panel in the reference stream, yet beta
+    scales all of C (sparse-matrix.cc:149-151): the native launch covers them too."""
+    rng = np.random.default_rng(5)
+    k, n, m = 40, 2000, 5
+    table = rng.uniform(-1, 1, 30).astype(np.float32)
+    dm = np.full((n, k), 255, np.uint8)          # Trans: S = dm^T is k x n
+    dm[300:520:7, ::3] = rng.integers(0, 30, (len(range(300, 520, 7)), len(range(0, k, 3))))
+    M = sm.SparseMatrix(dm, n, k, k, table, 30, sm.SblasTrans)
+    assert (M.NumRows(), M.NumCols()) == (k, n)
+    ref = oracle.RefModel(dm, n, k, k, table, 30, trans=True)
+    A = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+    C = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    for alpha, beta in ((1.3, 0.7), (1.0, 0.0), (0.0, 2.0), (1.0, 1.0)):
+        want = ref.add_mat_mat(A.reshape(-1), m, k, C.reshape(-1), n, alpha, beta)
+        for mm in (m, 1):
+            c_d = to_dev(C[:mm].reshape(-1).copy())
+            M.AddMatMat(to_dev(A[:mm].reshape(-1).copy()), mm, k, c_d, n, alpha, beta, algo="native")
+            assert bits_equal(to_host(c_d), want[: mm * n]), (alpha, beta, mm)
+
+
 @pytest.mark.parametrize("n,dens,m", [(16384, 0.001, 1), (4096, 0.25, 1), (2000, 0.05, 13),
                                       (3000, 0.6, 32)])
 def test_native_vs_oracle_larger(sm, n, dens, m):
