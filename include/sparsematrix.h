@@ -205,9 +205,10 @@ typedef struct sm_build_opts {
     int32_t ccsell;            /* column-chunked sliced-ELL (wide x): -1 auto, 0 never, 1 always
                                   (where no band layout is built and it applies)       */
     int32_t ccsell_chunk_log2; /* its column chunk, log2 columns (8..24), 0 = 20 (4 MiB of x) */
-    int32_t hot_cols;          /* skewed graphs (column relabeling built): the hottest this many
-                                  relabeled columns go through codebook bands with x in LDS,
-                                  the rest through the sliced ELL; 0 auto, -1 never        */
+    int32_t hot_cols;          /* skewed graphs (column relabeling built), opt-in: > 0 sends the
+                                  hottest this many relabeled columns through codebook bands
+                                  with x in LDS, the rest through the sliced ELL (within the
+                                  Sum|terms| bound); 0 / -1 never (slower on R-MAT 24)     */
     int32_t reserved_opts;
 } sm_build_opts;
 

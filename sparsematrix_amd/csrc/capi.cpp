@@ -683,23 +683,20 @@ sm_status upload_native(sm_matrix *m) {
 // through the codebook band kernel with their x staged in LDS (kernels_band2.hip) --
 // no gathers -- and the sliced ELL gathers only the rest.  A row then adds its hot
 // terms (in relabeled column order) before its cold ones (stored order): within the
-// Sum|terms| bound, deterministic.  AUTO takes H = 32768 when the hot prefix holds
-// >= 15 % of the terms and the graph has >= 2^18 rows; hot_cols = -1 never, > 0 forces H.
-constexpr int32_t kHotColsDefault = 32768;
-
+// Sum|terms| bound, deterministic.  Opt-in only (hot_cols > 0 sets H; 0 and -1 never):
+// measured on R-MAT scale 24 the split loses -- 2.71 ms at H = 32768, 2.16 ms at 8192,
+// 4.55 ms at 131072 against 1.66 ms for the codebook sliced ELL alone (the band pass
+// over 2^24 rows costs ~1.4 ms by itself; profiles/r03_rmat24_layout_ab.txt).
 sm_status upload_sell_layouts(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
     Plan &p = m->plan;
-    const int64_t H0 = m->opts.hot_cols < 0 ? 0 : m->opts.hot_cols > 0 ? m->opts.hot_cols : kHotColsDefault;
-    const bool try_hot = p.n_relabel > 0 && H0 > 0 && H0 < m->n_cols &&
-                         (m->opts.hot_cols > 0 || m->n_rows >= (1 << 18));
+    const int64_t H0 = m->opts.hot_cols > 0 ? m->opts.hot_cols : 0;
+    const bool try_hot = p.n_relabel > 0 && H0 > 0 && H0 < m->n_cols;
     if (!try_hot) return upload_sell(m, rp, col, val);
     const int64_t nnz = m->nnz, nr = m->n_rows;
     std::vector<int32_t> rcol((size_t)nnz);
     SM_TRY_HIP(hipMemcpy(rcol.data(), p.d_rcol, (size_t)nnz * 4, hipMemcpyDeviceToHost));
     int64_t hot = 0;
     for (int64_t e = 0; e < nnz; e++) hot += rcol[(size_t)e] < H0;
-    if (m->opts.hot_cols == 0 && (double)hot < 0.15 * (double)nnz)
-        return upload_sell(m, rp, rcol.data(), val, nnz, true);
     // Split every row into its hot part (sorted by relabeled column: the bands need
     // ascending columns) and its cold part (stored order).
     std::vector<int32_t> rph((size_t)nr + 1, 0), rpc((size_t)nr + 1, 0);

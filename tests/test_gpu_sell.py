@@ -152,15 +152,15 @@ def test_sell_special_values(sm):
 
 
 def test_sell_rmat_auto(sm):
-    """R-MAT scale 20 without band layouts: column relabeling + codebook sell.  With the
-    hot-column bands off (hot_cols = -1) rows of up to 2048 terms are bit-exact; AUTO
-    (the hottest relabeled columns as codebook bands first, then the sliced ELL) stays
+    """R-MAT scale 20 without band layouts: column relabeling + codebook sell, rows of up
+    to 2048 terms bit-exact (AUTO builds no hot-column bands); the opt-in split (the
+    hottest relabeled columns as codebook bands first, then the sliced ELL) stays
     within 1e-6 * sum|terms| on every row."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     rp_d, ci_d, va_d = synth.rmat_device(20, 16, seed=4)
     n = 1 << 20
-    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands", hot_cols=-1))
+    M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands"))
     info = M.info()
     assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
     assert info["hot_cols"] == 0, info
@@ -169,7 +169,7 @@ def test_sell_rmat_auto(sm):
     x = rng.uniform(-1, 1, n).astype(np.float32)
     y0 = rng.uniform(-1, 1, n).astype(np.float32)
     _check(M, rp, ci, va, x, y0, 1.0, 0.5, exact_max=2048)
-    H = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands"))
+    H = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(layout="no_bands", hot_cols=32768))
     hinfo = H.info()
     assert hinfo["hot_cols"] == 32768 and hinfo["col_relabel"] == 1, hinfo
     for alpha, beta in ((1.0, 0.5), (1.3, 0.0), (-0.7, 1.0)):
@@ -211,7 +211,7 @@ def test_config4_rmat24_auto_vs_oracle(sm):
     scale 24, edgefactor 16, seed 4 (263 M terms, rows up to 238 465 terms), AUTO =
     column relabeling + codebook sliced ELL with 2048-term segments.  Every row of up to
     2048 terms is bit-identical to the reference order (oracle), the longer rows (their
-    segment sums added in order) within 1e-6 * sum|terms|."""
+    segment sums added in order) and the opt-in hot-column split within 1e-6 * sum|terms|."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     rp_d, ci_d, va_d = synth.rmat_device(24, 16, seed=4)
@@ -219,9 +219,9 @@ def test_config4_rmat24_auto_vs_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n)
     info = M.info()
     assert info["sell_slices"] > 0 and info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
-    assert info["max_row_nnz"] > 2048 and info["hot_cols"] > 0, info
-    E = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(hot_cols=-1))
-    assert E.info()["hot_cols"] == 0
+    assert info["max_row_nnz"] > 2048 and info["hot_cols"] == 0, info
+    E = sm.SparseMatrix.from_csr(rp_d, ci_d, va_d, n, opts=dict(hot_cols=32768))
+    assert E.info()["hot_cols"] == 32768
     g = torch.Generator(device="cuda").manual_seed(4)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -236,9 +236,9 @@ def test_config4_rmat24_auto_vs_oracle(sm):
     want = oracle.csr_spmv_mt(rp, ci, va, xh, y0h, 1.0, 0.5, threads=16)
     lens = np.diff(rp.astype(np.int64))
     short = lens <= 2048
-    # without the hot bands: every row of <= 2048 terms in the reference's order
-    assert np.array_equal(bits(got_e[short]), bits(want[short]))
-    # AUTO (hot bands, then the sliced ELL), and the long rows: the Sum|terms| bound
+    # AUTO: every row of <= 2048 terms in the reference's order
+    assert np.array_equal(bits(got[short]), bits(want[short]))
+    # the opt-in hot bands, and the long rows: the Sum|terms| bound
     _, absum = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, xh, y0h, 1.0, 0.5)
     assert_terms_close(got, want, absum)
     assert_terms_close(got_e, want, absum)
