@@ -4,144 +4,266 @@
 // entry, fillers included) are decoded in parallel and applied, bit-identical to the
 // reference for every output.
 //
-// Grid: one workgroup per (panel, group of 64 output columns, group of 4 rows of A);
-// 256 threads, thread (cl, il) owns output C[i][col] (col = panel col_off + 64 g + cl,
-// i = 4 ig + il) and keeps it in a register for the whole kernel.  The workgroup walks
-// its panel's stream in chunks of 4096 entries, in order:
-//   1. decode   each thread loads 16 consecutive delta bytes and ids (one 16-byte load
-//               each), sums its deltas, and a wave prefix scan (DPP row shifts through
-//               __shfl_up) plus a 4-wave carry in LDS turns them into in-panel offsets
-//               off = running sum (kernel.cc:780-782), continued from the previous chunk;
-//   2. bucket   entries with id < T and a column in the group go to per-column lists in
-//               LDS (count, prefix over 64 columns, place); a column's entries in one
-//               chunk lie in distinct S-rows, so sorting each short list by row restores
-//               the stream order;
-//   3. apply    thread (cl, il) adds a[i][row] * fl(table[id] * alpha) for its column's
-//               entries in ascending row, separate roundings (kernel.cc:791, 568-582).
-// Across chunks the entries of a column keep ascending rows, so each output receives
-// its terms in exactly the reference's order after beta (kernel.cc:10-29).
+// Grid: (panel, group of 64 output columns, group of R rows of A), 256 threads.  Output
+// C[i][col] (col = panel col_off + 64 g + c, i = i0 + il) lives in a register of thread
+// c + 64 il for the whole kernel.  The workgroup walks its panel's stream in batches of
+// 4096 entries (16 per thread: one 16-byte load of deltas, one of ids; the next batch's
+// loads fly while this one is processed):
+//   1. decode  each thread sums its 16 deltas; a wave prefix scan, the wave totals and
+//              the carry of earlier batches give every entry its in-panel offset
+//              (kernel.cc:780-782): row = off >> 8, column = off & 255.  m = 1: the x
+//              value of every live entry is loaded now, so its latency hides behind 2-3;
+//   2. mark    live entries (id < T, kernel.cc:782; column in the group) set bit
+//              (row - row of the carry) in their column's bitmap -- a batch spans at most
+//              4082 rows (deltas <= 255), 128 words per column;
+//   3. rank    4 threads per column prefix-sum the popcounts of a quarter of its words
+//              each; one wave turns the quarter totals into list bases (a scan over the
+//              64 columns); an entry's slot is its column's base + the popcount of the
+//              bits below its own = its rank by row, so every list is in stream order;
+//   4. apply   thread (c, il) adds a[i][row] * fl(table[id] * alpha) over column c's
+//              list in order, separate roundings (kernel.cc:791, 568-582): m = 1 from the
+//              x values placed in LDS, m > 1 loading 8 entries' A values at a time.
+// Across batches a column's rows keep ascending, so each output receives its terms in
+// exactly the reference's order after beta (kernel.cc:10-29, sparse-matrix.cc:149-151).
 #include "sm_internal.h"
+
+#include <cstdio>
 
 namespace smamd {
 namespace {
 
 constexpr int kNatThreads = 256;
-constexpr int kNatPer = 16;                         // entries per thread per chunk
-constexpr int kNatChunk = kNatThreads * kNatPer;    // 4096
-constexpr int kNatCols = 64;                        // output columns per workgroup
-constexpr int kNatRows = kNatThreads / kNatCols;    // rows of A per workgroup
+constexpr int kNatPer = 16;                          // entries per thread per batch
+constexpr int kNatBatch = kNatThreads * kNatPer;     // 4096
+constexpr int kNatCols = 64;                         // output columns per workgroup
+constexpr int kNatWords = 128;                       // bitmap words per column (4096 rows)
+constexpr int kNatStride = kNatWords + 4;            // word w of column c at c*132 + w + w/32:
+                                                     // the 4 quarter readers of one column,
+                                                     // and adjacent columns, on distinct banks
+__device__ __forceinline__ int32_t bit_index(int32_t c, int32_t w) { return c * kNatStride + w + (w >> 5); }
 
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v, int lane) {
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const int32_t u = __shfl_up(v, s, 64);
+        if (lane >= s) v += u;
+    }
+    return v;
+}
+
+// PROF (development builds, SM_NAT_PROF): thread 0 of every workgroup adds the cycles
+// (s_memtime) of each phase into prof[0..7].
+// RT: rows of A per thread (rows i0 + il + 4 j, j < RT); X1: m = 1, the x values are
+// loaded at decode and placed in the lists (only the first wave applies).
+template <int RT, bool X1, bool PROF>
 __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
     const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
     const int64_t *__restrict__ pbeg, const int64_t *__restrict__ pend,
     const int32_t *__restrict__ pcol, const float *__restrict__ table, int32_t T, int32_t n,
     int32_t m, const float *__restrict__ a, int32_t lda, float *__restrict__ c, int32_t ldc,
-    float alpha, float beta) {
+    float alpha, float beta, unsigned long long *__restrict__ prof) {
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tk = PROF ? clock64() : 0;
+    auto mark_phase = [&](int k) {
+        if constexpr (PROF) {
+            const unsigned long long now = clock64();
+            ph[k] += now - tk;
+            tk = now;
+        }
+    };
+    constexpr int kDummyWord = kNatCols * kNatStride;   // dead entries OR 0 into it
     __shared__ float tab[256];
+    __shared__ uint32_t bits[kNatCols * kNatStride + 1];
+    __shared__ uint16_t wbase[kNatCols * kNatStride + 1];
+    __shared__ int32_t qbase[kNatCols * 4];          // quarter counts, then list bases
+    __shared__ int32_t cend[kNatCols];
     __shared__ int32_t wsum[kNatThreads / 64];
-    __shared__ int32_t cnt[kNatCols], base[kNatCols + 1], cur[kNatCols];
-    __shared__ int32_t lrow[kNatChunk];
-    __shared__ uint8_t lid[kNatChunk];
+    __shared__ uint32_t lent[kNatBatch + 1];         // X1: x value bits; else the row
+    __shared__ uint8_t lid[kNatBatch + 4];           // (+1: the dead entries' slot)
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int32_t p = blockIdx.x, g = blockIdx.y, ig = blockIdx.z;
-    const int cl = t & (kNatCols - 1), il = t / kNatCols;
+    const int32_t p = blockIdx.x, g = blockIdx.y;
+    const int32_t i0 = blockIdx.z * 4 * RT;
+    const int cl = t & (kNatCols - 1), il = t >> 6;  // apply role: column, first row of A
+    const int qc = t >> 2, qq = t & 3;               // rank role: column, quarter of its words
     const int32_t col = pcol[p] + g * kNatCols + cl;
-    const int32_t i = ig * kNatRows + il;
-    const bool own = col < n && g * kNatCols + cl < 256 && i < m;
+    const bool own = col < n && (!X1 || il == 0);
     tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
-    float acc = 0.0f;
-    if (own) {
-        acc = c[(int64_t)i * ldc + col];
-        if (beta != 1.0f) acc = __fmul_rn(acc, beta);
+    for (int w = t; w <= kDummyWord; w += kNatThreads) bits[w] = 0u;
+    float acc[RT];
+#pragma unroll
+    for (int j = 0; j < RT; ++j) {
+        const int32_t i = i0 + il + 4 * j;
+        acc[j] = 0.0f;
+        if (own && i < m) {
+            acc[j] = c[(int64_t)i * ldc + col];
+            if (beta != 1.0f) acc[j] = __fmul_rn(acc[j], beta);
+        }
     }
     const int64_t e_beg = pbeg[p], e_end = pend[p];
-    int32_t carry = 0;
-    for (int64_t e0 = e_beg; e0 < e_end; e0 += kNatChunk) {
-        // 1. decode: 16 entries per thread, in-panel offsets by a workgroup prefix sum.
+    auto load = [&](int64_t e0, uint4 &dv, uint4 &iv) {
         const int64_t e = e0 + (int64_t)t * kNatPer;
-        uint8_t d[kNatPer], id[kNatPer];
-        if (e + kNatPer <= e_end && ((e & 15) == 0)) {
-            const uint4 dv = *reinterpret_cast<const uint4 *>(pos + e);
-            const uint4 iv = *reinterpret_cast<const uint4 *>(val + e);
-            __builtin_memcpy(d, &dv, 16);
-            __builtin_memcpy(id, &iv, 16);
+        if (e + kNatPer <= e_end) {   // panel runs start 16-byte aligned (upload_native)
+            dv = *reinterpret_cast<const uint4 *>(pos + e);
+            iv = *reinterpret_cast<const uint4 *>(val + e);
         } else {
+            uint8_t d[kNatPer], id[kNatPer];
 #pragma unroll
             for (int k = 0; k < kNatPer; ++k) {
                 const bool in = e + k < e_end;
                 d[k] = in ? pos[e + k] : 0;
-                id[k] = in ? val[e + k] : 255;
+                id[k] = in ? val[e + k] : 255;   // >= T: skipped
             }
+            __builtin_memcpy(&dv, d, 16);
+            __builtin_memcpy(&iv, id, 16);
         }
+    };
+    uint4 dv_n = {0, 0, 0, 0}, iv_n = {0, 0, 0, 0};
+    if (e_beg < e_end) load(e_beg, dv_n, iv_n);
+    int32_t carry = 0;
+    __syncthreads();
+    mark_phase(0);
+    for (int64_t e0 = e_beg; e0 < e_end; e0 += kNatBatch) {
+        uint8_t d[kNatPer], id[kNatPer];
+        __builtin_memcpy(d, &dv_n, 16);
+        __builtin_memcpy(id, &iv_n, 16);
+        if (e0 + kNatBatch < e_end) load(e0 + kNatBatch, dv_n, iv_n);   // next batch in flight
+        // 1. decode
         int32_t tot = 0;
 #pragma unroll
         for (int k = 0; k < kNatPer; ++k) tot += d[k];
-        int32_t incl = tot;   // inclusive scan of the thread totals across the wave
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {
-            const int32_t v = __shfl_up(incl, s, 64);
-            if (lane >= s) incl += v;
-        }
+        const int32_t incl = wave_incl_scan(tot, lane);
         if (lane == 63) wsum[wave] = incl;
-        if (t < kNatCols) cnt[t] = 0;
         __syncthreads();
-        int32_t before = carry;
-        for (int w = 0; w < wave; ++w) before += wsum[w];
-        int32_t chunk_total = 0;
+        mark_phase(1);
+        int32_t off = carry + incl - tot;
+        int32_t batch_total = 0;
 #pragma unroll
-        for (int w = 0; w < kNatThreads / 64; ++w) chunk_total += wsum[w];
-        int32_t off = before + incl - tot;
-        int32_t offs[kNatPer];
-        bool live[kNatPer];
+        for (int w = 0; w < kNatThreads / 64; ++w) {
+            if (w < wave) off += wsum[w];
+            batch_total += wsum[w];
+        }
+        const int32_t row_lo = carry >> 8;
+        carry += batch_total;
+        const int32_t span_words = (((carry >> 8) - row_lo) >> 5) + 1;   // <= 128
+        // 2. mark (branch-free: dead entries OR 0 into the dummy word); rr = column << 16
+        // | row - row_lo, or -1 for a dead entry
+        int32_t rr[kNatPer];
+        float xv[kNatPer];
 #pragma unroll
         for (int k = 0; k < kNatPer; ++k) {
             off += d[k];
-            offs[k] = off;
-            const int32_t pc = off & 255;
-            live[k] = id[k] < T && (pc >> 6) == g;   // fillers carry id T
-            if (live[k]) atomicAdd(&cnt[pc & (kNatCols - 1)], 1);
-        }
-        carry += chunk_total;
-        __syncthreads();
-        // 2. bucket: column lists in LDS (placement order arbitrary, sorted by row below).
-        if (t == 0) {
-            int32_t s = 0;
-            for (int q = 0; q < kNatCols; ++q) { base[q] = s; cur[q] = s; s += cnt[q]; }
-            base[kNatCols] = s;
+            const int32_t pc = off & 255, r = (off >> 8) - row_lo;
+            const bool live = id[k] < T && (pc >> 6) == g;
+            if constexpr (X1) {   // m = 1: row 0 of A, live entries only
+                xv[k] = 0.0f;
+                if (live) xv[k] = a[off >> 8];
+            }
+            const int32_t wi = live ? bit_index(pc & 63, r >> 5) : kDummyWord;
+            atomicOr(&bits[wi], live ? 1u << (r & 31) : 0u);
+            rr[k] = live ? ((pc & 63) << 16) | r : -1;
         }
         __syncthreads();
+        mark_phase(2);
+        // 3. rank: quarter-local word prefix sums (thread (qc, qq): words 32 qq .. 32 qq + 31)
+        {
+            int32_t cnt = 0;
+            const int32_t w_hi = min(32 * qq + 32, span_words);
+            for (int32_t w0 = 32 * qq; w0 < w_hi; w0 += 8) {
+                uint32_t b[8];
 #pragma unroll
-        for (int k = 0; k < kNatPer; ++k) {
-            if (!live[k]) continue;
-            const int32_t slot = atomicAdd(&cur[offs[k] & (kNatCols - 1)], 1);
-            lrow[slot] = offs[k] >> 8;
-            lid[slot] = id[k];
+                for (int j = 0; j < 8; ++j) b[j] = w0 + j < w_hi ? bits[bit_index(qc, w0 + j)] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (w0 + j < w_hi) wbase[bit_index(qc, w0 + j)] = (uint16_t)cnt;
+                    cnt += __popc(b[j]);
+                }
+            }
+            qbase[t] = cnt;   // t = 4 qc + qq
         }
         __syncthreads();
-        if (il == 0) {   // insertion sort of the column's list by S-row (rows are distinct)
-            for (int32_t s = base[cl] + 1; s < base[cl + 1]; ++s) {
-                const int32_t r = lrow[s];
-                const uint8_t q = lid[s];
-                int32_t u = s - 1;
-                while (u >= base[cl] && lrow[u] > r) {
-                    lrow[u + 1] = lrow[u];
-                    lid[u + 1] = lid[u];
-                    --u;
-                }
-                lrow[u + 1] = r;
-                lid[u + 1] = q;
+        mark_phase(3);
+        if (wave == 0) {   // lane = column: quarter bases, then a scan over the columns
+            int32_t q4[4], ctot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                q4[q] = qbase[4 * lane + q];
+                ctot += q4[q];
+            }
+            int32_t b = wave_incl_scan(ctot, lane) - ctot;
+            cend[lane] = b + ctot;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                qbase[4 * lane + q] = b;
+                b += q4[q];
             }
         }
         __syncthreads();
-        // 3. apply, in ascending row.
-        if (own && alpha != 0.0f) {
-            const float *ai = a + (int64_t)i * lda;
-            for (int32_t s = base[cl]; s < base[cl + 1]; ++s)
-                acc = __fadd_rn(acc, __fmul_rn(ai[lrow[s]], tab[lid[s]]));
+        mark_phase(4);
+        // place (branch-free: dead entries write the spare slot)
+#pragma unroll
+        for (int k = 0; k < kNatPer; ++k) {
+            const bool live = rr[k] >= 0;
+            const int32_t q = live ? rr[k] >> 16 : 0, r = live ? rr[k] & 0xFFFF : 0;
+            const int32_t bi = live ? bit_index(q, r >> 5) : kDummyWord;
+            const int32_t rank = qbase[4 * q + (r >> 10)] + wbase[bi] +
+                                 __popc(bits[bi] & ((1u << (r & 31)) - 1u));
+            const int32_t slot = live ? rank : kNatBatch;
+            lent[slot] = X1 ? __float_as_uint(xv[k]) : (uint32_t)(r + row_lo);
+            lid[slot] = id[k];
         }
         __syncthreads();
+        mark_phase(5);
+        // 4. apply, in ascending row, 8 entries' reads ahead of their additions; the
+        // quarter readers clear their words meanwhile
+        if (X1 && own) {   // x values already in the list
+            const int32_t s0 = qbase[4 * cl], s1 = cend[cl];
+            for (int32_t s = s0; s < s1; ++s)
+                acc[0] = __fadd_rn(acc[0], __fmul_rn(__uint_as_float(lent[s]), tab[lid[s]]));
+        } else if (own) {
+            const int32_t s0 = qbase[4 * cl], s1 = cend[cl];
+            for (int32_t s = s0; s < s1; s += 8) {
+                float tv[8], av[8][RT];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int32_t sj = s + j < s1 ? s + j : kNatBatch;
+                    const uint32_t e = lent[sj];
+                    tv[j] = tab[lid[sj]];
+#pragma unroll
+                    for (int q = 0; q < RT; ++q) {
+                        const int32_t i = i0 + il + 4 * q;
+                        if constexpr (X1) av[j][q] = __uint_as_float(e);
+                        else av[j][q] = s + j < s1 && i < m ? a[(int64_t)i * lda + e] : 0.0f;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const bool in = s + j < s1;
+#pragma unroll
+                    for (int q = 0; q < RT; ++q) {
+                        const float sum = __fadd_rn(acc[q], __fmul_rn(av[j][q], tv[j]));
+                        acc[q] = in ? sum : acc[q];
+                    }
+                }
+            }
+        }
+        {
+            const int32_t w_hi = min(32 * qq + 32, span_words);
+            for (int32_t w = 32 * qq; w < w_hi; ++w) bits[bit_index(qc, w)] = 0u;
+        }
+        __syncthreads();
+        mark_phase(6);
     }
-    if (own) c[(int64_t)i * ldc + col] = acc;
+#pragma unroll
+    for (int j = 0; j < RT; ++j) {
+        const int32_t i = i0 + il + 4 * j;
+        if (own && i < m) c[(int64_t)i * ldc + col] = acc[j];
+    }
+    if constexpr (PROF) {
+        if (t == 0) {
+            ph[7] = 1;
+            for (int k = 0; k < 8; ++k) atomicAdd(prof + k, ph[k]);
+        }
+    }
 }
 
 }  // namespace
@@ -151,12 +273,43 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
     const int32_t P = beta != 1.0f ? nd.n_all : nd.n_panels;   // empty blocks only scale
     if (P <= 0 || m <= 0) return hipSuccess;
     if (!nd.d_pos || !nd.d_val || !nd.d_beg || !nd.d_end || !nd.d_col || !nd.d_table ||
-        nd.table_size < 0 || nd.table_size > 255)
+        nd.table_size < 0 || nd.table_size > 255 || nd.s_rows >= ((int64_t)1 << 23))
         return hipErrorInvalidValue;
-    const dim3 grid((unsigned)P, 256 / kNatCols, (unsigned)((m + kNatRows - 1) / kNatRows));
-    hipLaunchKernelGGL(native_addmatmat_kernel, grid, dim3(kNatThreads), 0, s, nd.d_pos, nd.d_val,
-                       nd.d_beg, nd.d_end, nd.d_col, nd.d_table, nd.table_size,
-                       (int32_t)nd.s_cols, m, a, lda, c, ldc, alpha, beta);
+    // m = 1: x values carried in the lists; m > 1: RT rows of A per thread, 4 RT per
+    // workgroup (one decode serves them all), at most 8.
+    const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;
+    const dim3 grid((unsigned)P, 256 / kNatCols, (unsigned)((m + 4 * RT - 1) / (4 * RT)));
+#define SM_NAT(RR, XX, PP, PTR)                                                               \
+    hipLaunchKernelGGL((native_addmatmat_kernel<RR, XX, PP>), grid, dim3(kNatThreads), 0, s,  \
+                       nd.d_pos, nd.d_val, nd.d_beg, nd.d_end, nd.d_col, nd.d_table,          \
+                       nd.table_size, (int32_t)nd.s_cols, m, a, lda, c, ldc, alpha, beta, PTR)
+#define SM_NAT_ALL(PP, PTR)                                                                   \
+    do {                                                                                      \
+        if (m == 1) SM_NAT(1, true, PP, PTR);                                                 \
+        else if (RT == 1) SM_NAT(1, false, PP, PTR);                                          \
+        else if (RT == 2) SM_NAT(2, false, PP, PTR);                                          \
+        else if (RT == 4) SM_NAT(4, false, PP, PTR);                                          \
+        else SM_NAT(8, false, PP, PTR);                                                       \
+    } while (0)
+#ifdef SM_DEV
+    if (dev_env("SM_NAT_PROF")) {   // per-phase cycles, summed over workgroups, to stderr
+        unsigned long long *d = nullptr, h[8] = {};
+        if (hipMalloc(&d, sizeof(h)) != hipSuccess) return hipErrorOutOfMemory;
+        (void)hipMemsetAsync(d, 0, sizeof(h), s);
+        SM_NAT_ALL(true, d);
+        (void)hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(d);
+        const double wgs = (double)h[7];
+        fprintf(stderr, "native prof (kcycles per workgroup, %.0f wgs): init %.2f scan %.2f mark %.2f "
+                "rank1 %.2f rank2 %.2f place %.2f apply %.2f\n", wgs, h[0] / wgs / 1e3, h[1] / wgs / 1e3,
+                h[2] / wgs / 1e3, h[3] / wgs / 1e3, h[4] / wgs / 1e3, h[5] / wgs / 1e3, h[6] / wgs / 1e3);
+        return hipGetLastError();
+    }
+#endif
+    SM_NAT_ALL(false, nullptr);
+#undef SM_NAT_ALL
+#undef SM_NAT
     return hipGetLastError();
 }
 
