@@ -33,13 +33,25 @@
 #include "xband.h"
 #include "xband_dev.h"
 
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
+#include <algorithm>
 #include <type_traits>
 
 namespace smamd {
 namespace {
 
 constexpr int kB2Threads = 1024;
+#ifdef SM_DEV
+// ABL & 1024 (development builds): lane 0 of every wave adds the cycles (s_memtime) of
+// each phase of the band loop here: prologue, x store (its wait), apply, entry load
+// issue, barrier, epilogue, bands, waves.
+__device__ unsigned long long g_b2_prof[8];
+// ABL & 2048: wall clock (s_memrealtime, 100 MHz) of every tile's start, loop end and
+// finish, from thread 0.
+__device__ unsigned long long g_b2_ts[3 * 4096];
+#endif
 // Lookaheads (bands) of the x windows and of the entries; development builds
 // override them (tools/r2_ab.sh).
 #ifndef SM_CB_XAHEAD
@@ -91,7 +103,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
-    int32_t *__restrict__ ctl, float alpha, float beta) {
+    int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : kB2Wide;
     constexpr int BROWS = G.block_rows;
     constexpr int W = G.window;
@@ -140,7 +152,30 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     __shared__ float tab[CB ? 256 * kTabCopies : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int32_t t = blockIdx.x;
+    constexpr bool kProf = (ABL & 1024) != 0;
+    constexpr bool kTs = (ABL & 2048) != 0;
+#ifdef SM_DEV
+    if constexpr (kTs) {
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x] = wall_clock64();
+    }
+#endif
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tk = kProf ? clock64() : 0;
+    auto mark_phase = [&](int k) {
+        if constexpr (kProf) {
+            const unsigned long long now = clock64();
+            ph[k] += now - tk;
+            tk = now;
+        }
+    };
+    // Tile of this workgroup.  xcd_map: workgroup i runs on XCD i % 8 (dispatch round
+    // robin), so tile = the i / 8-th of XCD (i % 8)'s contiguous range of tiles: the
+    // slabs of one row block share an XCD and their hand-off stays in its L2.
+    int32_t t = blockIdx.x;
+    if (xcd_map) {
+        const int32_t G = gridDim.x, xc = t & 7, k = t >> 3;
+        t = xc * (G >> 3) + min(xc, G & 7) + k;
+    }
     const int32_t b = t / n_slabs;
     const int32_t slab = t - b * n_slabs;
     if (!(ABL & 8)) handoff_started(ctl + (int64_t)b * kCtlWords, n_slabs);
@@ -424,6 +459,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // dummies write nothing but the x buffers nobody reads any more (band2: and the
     // scratch slots).
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
+    mark_phase(0);
     for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -435,6 +471,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 load_x(q + AX, X[u % AX]);
                 store_x((u + 1) & 1, X[(u + 1) % AX]);
             }
+            if constexpr (kProf) {   // the x store's wait, made visible
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                mark_phase(1);
+            }
             if constexpr (kEarly) E[(u + AE) % ER] = load_e(q + AE);
             if constexpr (ABL & 1) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
@@ -443,13 +483,40 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             } else {
                 apply_b2(xs[u & 1], E[u % ER]);
             }
+            if constexpr (kProf) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                mark_phase(2);
+            }
             if constexpr (!kEarly) E[u % ER] = load_e(q + AE);
+            mark_phase(3);
             // kDma: window q+1 landed (in-order retirement); the entry load just issued flies.
             if constexpr (kDma) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
             if (!(ABL & 512) && q < nb) __syncthreads();
+            mark_phase(4);
         }
     }
+    if constexpr (kProf) {
+        ph[6] = (unsigned long long)nb;
+        ph[7] = 1;
+    }
+#ifdef SM_DEV
+    if constexpr (kTs) {
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x + 1] = wall_clock64();
+    }
+#endif
 
+    auto flush_prof = [&]() {
+#ifdef SM_DEV
+        if constexpr (kTs) {
+            if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x + 2] = wall_clock64();
+        }
+        if constexpr (kProf) {
+            mark_phase(5);
+            if (lane == 0)
+                for (int k = 0; k < 8; ++k) atomicAdd(&g_b2_prof[k], ph[k]);
+        }
+#endif
+    };
     if (n_slabs == 1 || (ABL & 8)) {
         const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
 #pragma unroll
@@ -458,6 +525,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if (i < nv) *reinterpret_cast<float4 *>(y + r0 + i) = *reinterpret_cast<const float4 *>(&yacc[i]);
         }
         for (int32_t i = nv + tid; i < nr; i += kB2Threads) y[r0 + i] = yacc[i];
+        flush_prof();
         return;
     }
     int32_t *s_word = s_word_b2;
@@ -467,6 +535,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
     slab_handoff<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
                              nr, slab, n_slabs, y_vec);
+    flush_prof();
 }
 
 }  // namespace
@@ -484,10 +553,15 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         (xb.n_slabs > 1 && (!xb.d_partials || !xb.d_tickets)))
         return hipErrorInvalidValue;
     const dim3 grid((unsigned)((int64_t)xb.n_blocks * xb.n_slabs)), block(kB2Threads);
+    int32_t xcd_map = 0;
+#ifdef SM_DEV
+    if (const char *e = dev_env("SM_B2_XCDMAP")) xcd_map = atoi(e);
+#endif
 #define SM_B2(A, P, C, T)                                                                      \
     hipLaunchKernelGGL((spmv_band2_kernel<A, P, C, T>), grid, block, 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,   \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta,  \
+                       xcd_map)
 #ifdef SM_DEV
     // Development builds: ablations (SM_BAND2_ABLATE, results wrong) and the wave
     // priority (SM_BAND2_PRIO) of DESIGN.md §3.4b's measurements.
@@ -527,6 +601,54 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         case 512: SM_B2(512, 2, true, false); break;
         case 516: SM_B2(516, 2, true, false); break;
         case 513: SM_B2(513, 2, true, false); break;
+        case 1024: {
+            unsigned long long h[8] = {};
+            void *sym = nullptr;
+            if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_prof)) != hipSuccess) return hipErrorInvalidValue;
+            (void)hipMemsetAsync(sym, 0, sizeof(h), s);
+            SM_B2(1024, 2, true, false);
+            (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double w = (double)h[7], bands = (double)h[6] / w;
+            fprintf(stderr, "cband prof (cycles per wave; %.0f waves, %.1f bands): prologue %.0f | per band: "
+                    "x store %.0f apply %.0f e-load %.0f barrier %.0f | epilogue %.0f\n", w, bands,
+                    h[0] / w, h[1] / w / bands, h[2] / w / bands, h[3] / w / bands, h[4] / w / bands, h[5] / w);
+            break;
+        }
+        case 2048: {
+            const int nt = (int)std::min<int64_t>(grid.x, 4096);
+            std::vector<unsigned long long> h((size_t)3 * nt);
+            void *sym = nullptr;
+            if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
+            SM_B2(2048, 2, true, false);
+            (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            unsigned long long t0 = ~0ull;
+            for (int i = 0; i < nt; i++) t0 = std::min(t0, h[3 * i]);
+            std::vector<double> st(nt), lp(nt), ep(nt), en(nt);
+            for (int i = 0; i < nt; i++) {
+                st[i] = (h[3 * i] - t0) * 0.01;                 // us (100 MHz)
+                lp[i] = (h[3 * i + 1] - h[3 * i]) * 0.01;
+                ep[i] = (h[3 * i + 2] - h[3 * i + 1]) * 0.01;
+                en[i] = (h[3 * i + 2] - t0) * 0.01;
+            }
+            auto pr = [](const char *nm, std::vector<double> v) {
+                std::sort(v.begin(), v.end());
+                const size_t k = v.size();
+                fprintf(stderr, "  %-9s min %6.2f p10 %6.2f p50 %6.2f p90 %6.2f max %6.2f us\n", nm, v[0],
+                        v[k / 10], v[k / 2], v[9 * k / 10], v[k - 1]);
+            };
+            fprintf(stderr, "cband tile timeline (%d tiles):\n", nt);
+            pr("start", st);
+            pr("loop", lp);
+            pr("epilogue", ep);
+            pr("end", en);
+            if (dev_env("SM_B2_TS_DUMP")) {
+                for (int i = 0; i < nt; i++)
+                    fprintf(stderr, "  tile %4d start %6.2f loop %6.2f epi %6.2f\n", i, st[i], lp[i], ep[i]);
+            }
+            break;
+        }
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
