@@ -125,6 +125,12 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.nat.d_end);
     (void)hipFree(m->plan.nat.d_col);
     (void)hipFree(m->plan.nat.d_table);
+    (void)hipFree(m->plan.nat.d_pbatch);
+    (void)hipFree(m->plan.nat.d_bpanel);
+    (void)hipFree(m->plan.nat.d_bcarry);
+    (void)hipFree(m->plan.nat.d_boff);
+    (void)hipFree(m->plan.nat.d_lists);
+    (void)hipFree(m->plan.nat.d_hdr);
     free_xband_dev(m->plan.hot);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
@@ -675,6 +681,44 @@ sm_status upload_native(sm_matrix *m) {
     d.s_cols = m->s_cols;
     d.n_panels = (int32_t)P;
     d.n_all = (int32_t)Pc;
+    // Batch metadata of the two-kernel form: the carry before each batch and the live
+    // entries of each (batch, group) -- derived from the stream once, as the panel bounds are.
+    std::vector<int32_t> pbatch(Pc + 1, 0), bpanel, bcarry, boff;
+    int64_t live_total = 0;
+    for (size_t p = 0; p < Pc; p++) {
+        pbatch[p] = (int32_t)bpanel.size();
+        int32_t carry = 0;
+        for (int64_t e0 = beg[p]; e0 < end[p]; e0 += kNatBatchEntries) {
+            bpanel.push_back((int32_t)p);
+            bcarry.push_back(carry);
+            int64_t live[4] = {0, 0, 0, 0};
+            const int64_t e1 = std::min<int64_t>(end[p], e0 + kNatBatchEntries);
+            for (int64_t e = e0; e < e1; e++) {
+                carry += pos[(size_t)e];
+                if (val[(size_t)e] < m->table_size) live[(carry & 255) >> 6]++;
+            }
+            for (int g = 0; g < 4; g++) {
+                boff.push_back((int32_t)live_total);
+                live_total += live[g];
+            }
+        }
+        d.max_panel_batches = std::max<int32_t>(d.max_panel_batches, (int32_t)bpanel.size() - pbatch[p]);
+    }
+    pbatch[Pc] = (int32_t)bpanel.size();
+    d.n_batches = (int32_t)bpanel.size();
+    if (live_total >= ((int64_t)1 << 31)) return SM_OK;   // fused kernel only
+    if (d.n_batches > 0 && d.max_panel_batches > kNatFusedBatches) {
+        SM_TRY_HIP(dev_alloc(&d.d_pbatch, (int64_t)Pc + 1, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_bpanel, (int64_t)d.n_batches, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_bcarry, (int64_t)d.n_batches, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_boff, (int64_t)d.n_batches * 4, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_lists, std::max<int64_t>(live_total, 1), m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_hdr, (int64_t)d.n_batches * 256, m->device_bytes));
+        SM_TRY_HIP(hipMemcpy(d.d_pbatch, pbatch.data(), (Pc + 1) * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_bpanel, bpanel.data(), bpanel.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_bcarry, bcarry.data(), bcarry.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_boff, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
+    }
     return SM_OK;
 }
 
@@ -830,6 +874,33 @@ std::unique_ptr<sm_matrix> new_matrix(int32_t device, const sm_build_opts *opts 
     return m;
 }
 
+}  // namespace
+
+namespace {
+// Launches that use the matrix's scratch (sm_internal.h: scratch_ready) run one after
+// the other on the device: the stream waits for the previous such launch's event, and
+// records it after its own (not while the stream is being captured into a graph).
+template <class F>
+hipError_t with_scratch(const sm_matrix *m, hipStream_t s, bool needed, F &&launch) {
+    if (!needed) return launch();
+    std::lock_guard<std::mutex> lk(m->scratch_mu);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    const bool ordered = cs == hipStreamCaptureStatusNone;
+    hipError_t e = hipSuccess;
+    if (ordered && !m->scratch_ready) e = hipEventCreateWithFlags(&m->scratch_ready, hipEventDisableTiming);
+    if (ordered && e == hipSuccess && m->scratch_recorded) e = hipStreamWaitEvent(s, m->scratch_ready, 0);
+    if (e != hipSuccess) return e;
+    e = launch();
+    if (ordered) {   // whatever was queued (also on a failed launch) uses the scratch
+        const hipError_t er = hipEventRecord(m->scratch_ready, s);
+        if (er == hipSuccess) m->scratch_recorded = true;
+        if (e == hipSuccess) e = er;
+    }
+    return e;
+}
+
+bool native_scratch(const NativeDev &nd) { return nd.d_lists && nd.max_panel_batches > kNatFusedBatches; }
 }  // namespace
 
 extern "C" {
@@ -1303,9 +1374,12 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     if (algo == SM_ALGO_NATIVE) {   // the reference stream: y = x * S (a = x, c = y, m = 1)
         if (!m->has_ref || (m->plan.nat.n_panels == 0 && m->nnz > 0))
             return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_NATIVE needs a matrix built from the dense index");
-        e = m->plan.nat.n_panels == 0 ? (beta != 1.0f ? launch_beta(y, 1, n, n, beta, s) : hipSuccess)
-                                      : launch_native_addmatmat(m->plan.nat, 1, x, (int32_t)m->n_cols, y,
-                                                                n, alpha, beta, s);
+        e = m->plan.nat.n_panels == 0
+                ? (beta != 1.0f ? launch_beta(y, 1, n, n, beta, s) : hipSuccess)
+                : with_scratch(m, s, native_scratch(m->plan.nat), [&] {
+                      return launch_native_addmatmat(m->plan.nat, 1, x, (int32_t)m->n_cols, y, n, alpha,
+                                                     beta, s);
+                  });
         e = after_launch(e, s, "sm_spmv native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv native");
     }
@@ -1443,7 +1517,9 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
             return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_NATIVE needs a matrix built from the dense index");
         e = mat->plan.nat.n_panels == 0
                 ? (beta != 1.0f ? launch_beta(c, m, (int32_t)n, ldc, beta, s) : hipSuccess)
-                : launch_native_addmatmat(mat->plan.nat, m, a, lda, c, ldc, alpha, beta, s);
+                : with_scratch(mat, s, native_scratch(mat->plan.nat), [&] {
+                      return launch_native_addmatmat(mat->plan.nat, m, a, lda, c, ldc, alpha, beta, s);
+                  });
         e = after_launch(e, s, "sm_addmatmat native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat native");
     }

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     constexpr bool kProf = (ABL & 1024) != 0;
-    constexpr bool kTs = (ABL & 2048) != 0;
+    [[maybe_unused]] constexpr bool kTs = (ABL & 2048) != 0;
 #ifdef SM_DEV
     if constexpr (kTs) {
         if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x] = wall_clock64();

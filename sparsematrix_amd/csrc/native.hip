@@ -266,6 +266,206 @@ __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
     }
 }
 
+// ---- two-kernel form (panels of more than kNatFusedBatches batches) --------------------
+// The fused kernel walks a panel's batches one after the other, so a long panel is one
+// workgroup's serial chain.  Here every (batch, column group) decodes at once -- its carry
+// (the offset before the batch) comes from the upload -- and writes each column's list,
+// in stream order, to d_lists; then one thread per output walks its column's lists batch
+// after batch.  m = 1: the list holds the term fl(x[row] * fl(table[id] * alpha))
+// itself (the same two roundings, kernel.cc:791 / 580-582); m > 1: row | id << 23.
+template <bool X1>
+__global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
+    const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
+    const int64_t *__restrict__ pbeg, const int64_t *__restrict__ pend,
+    const int32_t *__restrict__ pbatch, const int32_t *__restrict__ bpanel,
+    const int32_t *__restrict__ bcarry, const int32_t *__restrict__ boff,
+    const float *__restrict__ table, int32_t T, const float *__restrict__ x, float alpha,
+    uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr) {
+    constexpr int kDummyWord = kNatCols * kNatStride;
+    __shared__ float tab[256];
+    __shared__ uint32_t bits[kNatCols * kNatStride + 1];
+    __shared__ uint16_t wbase[kNatCols * kNatStride + 1];
+    __shared__ int32_t qbase[kNatCols * 4];
+    __shared__ int32_t wsum[kNatThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int qc = t >> 2, qq = t & 3;
+    const int32_t b = blockIdx.x, g = blockIdx.y;
+    const int32_t p = bpanel[b];
+    const int64_t e0 = pbeg[p] + (int64_t)(b - pbatch[p]) * kNatBatch, e_end = pend[p];
+    if (X1) tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
+    for (int w = t; w <= kDummyWord; w += kNatThreads) bits[w] = 0u;
+    uint8_t d[kNatPer], id[kNatPer];
+    {
+        const int64_t e = e0 + (int64_t)t * kNatPer;
+        if (e + kNatPer <= e_end) {   // 16-byte aligned (upload_native)
+            const uint4 dv = *reinterpret_cast<const uint4 *>(pos + e);
+            const uint4 iv = *reinterpret_cast<const uint4 *>(val + e);
+            __builtin_memcpy(d, &dv, 16);
+            __builtin_memcpy(id, &iv, 16);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kNatPer; ++k) {
+                const bool in = e + k < e_end;
+                d[k] = in ? pos[e + k] : 0;
+                id[k] = in ? val[e + k] : 255;
+            }
+        }
+    }
+    const int32_t carry = bcarry[b];
+    int32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kNatPer; ++k) tot += d[k];
+    const int32_t incl = wave_incl_scan(tot, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int32_t off = carry + incl - tot, batch_total = 0;
+#pragma unroll
+    for (int w = 0; w < kNatThreads / 64; ++w) {
+        if (w < wave) off += wsum[w];
+        batch_total += wsum[w];
+    }
+    const int32_t row_lo = carry >> 8;
+    const int32_t span_words = ((((carry + batch_total) >> 8) - row_lo) >> 5) + 1;   // <= 128
+    int32_t rr[kNatPer];
+    float xv[kNatPer];
+#pragma unroll
+    for (int k = 0; k < kNatPer; ++k) {
+        off += d[k];
+        const int32_t pc = off & 255, r = (off >> 8) - row_lo;
+        const bool live = id[k] < T && (pc >> 6) == g;
+        if constexpr (X1) {
+            xv[k] = 0.0f;
+            if (live) xv[k] = x[off >> 8];
+        }
+        const int32_t wi = live ? bit_index(pc & 63, r >> 5) : kDummyWord;
+        atomicOr(&bits[wi], live ? 1u << (r & 31) : 0u);
+        rr[k] = live ? ((pc & 63) << 16) | r : -1;
+    }
+    __syncthreads();
+    {
+        int32_t cnt = 0;
+        const int32_t w_hi = min(32 * qq + 32, span_words);
+        for (int32_t w0 = 32 * qq; w0 < w_hi; w0 += 8) {
+            uint32_t bw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bw[j] = w0 + j < w_hi ? bits[bit_index(qc, w0 + j)] : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (w0 + j < w_hi) wbase[bit_index(qc, w0 + j)] = (uint16_t)cnt;
+                cnt += __popc(bw[j]);
+            }
+        }
+        qbase[t] = cnt;
+    }
+    __syncthreads();
+    if (wave == 0) {   // lane = column: quarter bases, the column scan, the list header
+        int32_t q4[4], ctot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            q4[q] = qbase[4 * lane + q];
+            ctot += q4[q];
+        }
+        int32_t cb = wave_incl_scan(ctot, lane) - ctot;
+        hdr[((int64_t)b * 4 + g) * kNatCols + lane] = (uint32_t)cb | ((uint32_t)(cb + ctot) << 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            qbase[4 * lane + q] = cb;
+            cb += q4[q];
+        }
+    }
+    __syncthreads();
+    uint32_t *out = lists + boff[b * 4 + g];
+#pragma unroll
+    for (int k = 0; k < kNatPer; ++k) {
+        if (rr[k] < 0) continue;
+        const int32_t q = rr[k] >> 16, r = rr[k] & 0xFFFF;
+        const int32_t bi = bit_index(q, r >> 5);
+        const int32_t slot = qbase[4 * q + (r >> 10)] + wbase[bi] + __popc(bits[bi] & ((1u << (r & 31)) - 1u));
+        out[slot] = X1 ? __float_as_uint(__fmul_rn(xv[k], tab[id[k]]))
+                       : (uint32_t)(r + row_lo) | ((uint32_t)id[k] << 23);
+    }
+}
+
+// One thread per (column, RT rows of A); X1: one wave per (panel, group), the terms added.
+template <int RT, bool X1>
+__global__ __launch_bounds__(X1 ? 64 : kNatThreads) void native_apply_kernel(
+    const int32_t *__restrict__ pcol, const int32_t *__restrict__ pbatch,
+    const int32_t *__restrict__ boff, const uint32_t *__restrict__ lists,
+    const uint32_t *__restrict__ hdr, const float *__restrict__ table, int32_t T, int32_t n,
+    int32_t m, const float *__restrict__ a, int32_t lda, float *__restrict__ c, int32_t ldc,
+    float alpha, float beta) {
+    __shared__ float tab[X1 ? 1 : 256];
+    const int t = threadIdx.x, cl = t & 63, il = t >> 6;
+    const int32_t p = blockIdx.x, g = blockIdx.y;
+    const int32_t i0 = blockIdx.z * 4 * RT;
+    const int32_t col = pcol[p] + g * kNatCols + cl;
+    const bool own = col < n;
+    if constexpr (!X1) {
+        tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
+        __syncthreads();
+    }
+    float acc[RT];
+#pragma unroll
+    for (int j = 0; j < RT; ++j) {
+        const int32_t i = i0 + il + 4 * j;
+        acc[j] = 0.0f;
+        if (own && i < m) {
+            acc[j] = c[(int64_t)i * ldc + col];
+            if (beta != 1.0f) acc[j] = __fmul_rn(acc[j], beta);
+        }
+    }
+    const int32_t b0 = pbatch[p], b1 = pbatch[p + 1];
+    if (own && b0 < b1) {
+        uint32_t h = hdr[((int64_t)b0 * 4 + g) * kNatCols + cl];
+        int32_t o = boff[b0 * 4 + g];
+        for (int32_t b = b0; b < b1; ++b) {
+            const int32_t s0 = o + (int32_t)(h & 0xFFFF), s1 = o + (int32_t)(h >> 16);
+            if (b + 1 < b1) {   // the next batch's header, in flight meanwhile
+                h = hdr[((int64_t)(b + 1) * 4 + g) * kNatCols + cl];
+                o = boff[(b + 1) * 4 + g];
+            }
+            for (int32_t s = s0; s < s1; s += 8) {
+                uint32_t e[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) e[j] = lists[s + j < s1 ? s + j : s0];
+                if constexpr (X1) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float sum = __fadd_rn(acc[0], __uint_as_float(e[j]));
+                        acc[0] = s + j < s1 ? sum : acc[0];
+                    }
+                } else {
+                    float av[8][RT], tv[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int32_t row = (int32_t)(e[j] & 0x7FFFFFu);
+                        tv[j] = tab[e[j] >> 23];
+#pragma unroll
+                        for (int q = 0; q < RT; ++q) {
+                            const int32_t i = i0 + il + 4 * q;
+                            av[j][q] = s + j < s1 && i < m ? a[(int64_t)i * lda + row] : 0.0f;
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const bool in = s + j < s1;
+#pragma unroll
+                        for (int q = 0; q < RT; ++q) {
+                            const float sum = __fadd_rn(acc[q], __fmul_rn(av[j][q], tv[j]));
+                            acc[q] = in ? sum : acc[q];
+                        }
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RT; ++j) {
+        const int32_t i = i0 + il + 4 * j;
+        if (own && i < m) c[(int64_t)i * ldc + col] = acc[j];
+    }
+}
+
 }  // namespace
 
 hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *a, int32_t lda,
@@ -275,6 +475,35 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
     if (!nd.d_pos || !nd.d_val || !nd.d_beg || !nd.d_end || !nd.d_col || !nd.d_table ||
         nd.table_size < 0 || nd.table_size > 255 || nd.s_rows >= ((int64_t)1 << 23))
         return hipErrorInvalidValue;
+    if (nd.max_panel_batches > kNatFusedBatches && nd.d_lists) {
+        // Two kernels: decode every (batch, group) at once, then walk the lists.
+        const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;
+        if (nd.n_batches > 0) {
+            const dim3 dgrid((unsigned)nd.n_batches, 256 / kNatCols);
+            if (m == 1)
+                hipLaunchKernelGGL(native_decode_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                                   nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel, nd.d_bcarry,
+                                   nd.d_boff, nd.d_table, nd.table_size, a, alpha, nd.d_lists, nd.d_hdr);
+            else
+                hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                                   nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel, nd.d_bcarry,
+                                   nd.d_boff, nd.d_table, nd.table_size, a, alpha, nd.d_lists, nd.d_hdr);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        const dim3 agrid((unsigned)P, 256 / kNatCols, (unsigned)(m == 1 ? 1 : (m + 4 * RT - 1) / (4 * RT)));
+#define SM_NAT_APPLY(RR, XX)                                                                  \
+    hipLaunchKernelGGL((native_apply_kernel<RR, XX>), agrid, dim3(XX ? 64 : kNatThreads), 0, s, \
+                       nd.d_col, nd.d_pbatch, nd.d_boff, nd.d_lists, nd.d_hdr, nd.d_table,    \
+                       nd.table_size, (int32_t)nd.s_cols, m, a, lda, c, ldc, alpha, beta)
+        if (m == 1) SM_NAT_APPLY(1, true);
+        else if (RT == 1) SM_NAT_APPLY(1, false);
+        else if (RT == 2) SM_NAT_APPLY(2, false);
+        else if (RT == 4) SM_NAT_APPLY(4, false);
+        else SM_NAT_APPLY(8, false);
+#undef SM_NAT_APPLY
+        return hipGetLastError();
+    }
     // m = 1: x values carried in the lists; m > 1: RT rows of A per thread, 4 RT per
     // workgroup (one decode serves them all), at most 8.
     const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;

@@ -133,7 +133,20 @@ struct NativeDev {
     int32_t *d_col = nullptr;
     float *d_table = nullptr;         // table_size raw values
     int32_t table_size = 0;
+    // Two-kernel form (panels of more than kNatFusedBatches batches of 4096 entries):
+    // per batch its panel and the in-panel offset before it (the reference's running
+    // pos_offset, kernel.cc:780-781), per (batch, group of 64 columns) the start of its
+    // column lists in d_lists (4 bytes per live entry) and per (batch, group, column)
+    // the list's [begin, end) written by the decode kernel.
+    int32_t n_batches = 0, max_panel_batches = 0;
+    int32_t *d_pbatch = nullptr;      // n_all + 1: first batch of each panel
+    int32_t *d_bpanel = nullptr, *d_bcarry = nullptr;   // per batch
+    int32_t *d_boff = nullptr;        // per (batch, group)
+    uint32_t *d_lists = nullptr;      // live entries: m = 1 the term's bits, else row | id << 23
+    uint32_t *d_hdr = nullptr;        // per (batch, group, column): begin | end << 16
 };
+constexpr int kNatBatchEntries = 4096;
+constexpr int kNatFusedBatches = 2;   // panels of at most this many batches: one fused kernel
 
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built

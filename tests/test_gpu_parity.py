@@ -847,6 +847,33 @@ def test_native_beta_scales_columns_without_panels(sm):
             assert bits_equal(to_host(c_d), want[: mm * n]), (alpha, beta, mm)
 
 
+def test_native_two_streams(sm):
+    """The two-kernel native form keeps its column lists in the matrix: native calls on one
+    matrix from two streams at once are ordered on the device, every result equal to the
+    restated reference AddMatMat (oracle.RefModel), m = 1 and m = 5."""
+    torch = torch_dev()
+    rng = np.random.default_rng(77)
+    n = 3000
+    table = rng.uniform(-1, 1, 100).astype(np.float32)
+    dm = np.where(rng.random((n, n)) < 0.1, rng.integers(0, 100, (n, n)), 255).astype(np.uint8)
+    M = sm.SparseMatrix(dm, n, n, n, table, 100, sm.SblasTrans)
+    ref = oracle.RefModel(dm, n, n, n, table, 100, trans=True)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for m in (1, 5):
+        As = [rng.uniform(-1, 1, (m, n)).astype(np.float32) for _ in range(6)]
+        C0 = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+        want = [ref.add_mat_mat(A.reshape(-1), m, n, C0.reshape(-1), n, 1.3, 0.5) for A in As]
+        a_d = [to_dev(A.reshape(-1)) for A in As]
+        c_d = [to_dev(C0.reshape(-1)) for _ in As]
+        torch.cuda.synchronize()
+        for i in range(len(As)):
+            with torch.cuda.stream(streams[i % 2]):
+                M.AddMatMat(a_d[i], m, n, c_d[i], n, 1.3, 0.5, algo="native")
+        torch.cuda.synchronize()
+        for i in range(len(As)):
+            assert bits_equal(to_host(c_d[i]), want[i]), (m, i)
+
+
 @pytest.mark.parametrize("n,dens,m", [(16384, 0.001, 1), (4096, 0.25, 1), (2000, 0.05, 13),
                                       (3000, 0.6, 32)])
 def test_native_vs_oracle_larger(sm, n, dens, m):
