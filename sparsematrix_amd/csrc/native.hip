@@ -273,14 +273,23 @@ __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
 // in stream order, to d_lists; then one thread per output walks its column's lists batch
 // after batch.  m = 1: the list holds the term fl(x[row] * fl(table[id] * alpha))
 // itself (the same two roundings, kernel.cc:791 / 580-582); m > 1: row | id << 23.
-template <bool X1>
+template <bool X1, bool PROF = false>
 __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
     const int64_t *__restrict__ pbeg, const int64_t *__restrict__ pend,
     const int32_t *__restrict__ pbatch, const int32_t *__restrict__ bpanel,
     const int32_t *__restrict__ bcarry, const int32_t *__restrict__ boff,
     const float *__restrict__ table, int32_t T, const float *__restrict__ x, float alpha,
-    uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr) {
+    uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr, unsigned long long *__restrict__ prof = nullptr) {
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tk = PROF ? clock64() : 0;
+    auto mark_phase = [&](int k) {
+        if constexpr (PROF) {
+            const unsigned long long now = clock64();
+            ph[k] += now - tk;
+            tk = now;
+        }
+    };
     constexpr int kDummyWord = kNatCols * kNatStride;
     __shared__ float tab[256];
     __shared__ uint32_t bits[kNatCols * kNatStride + 1];
@@ -312,12 +321,14 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
         }
     }
     const int32_t carry = bcarry[b];
+    mark_phase(0);
     int32_t tot = 0;
 #pragma unroll
     for (int k = 0; k < kNatPer; ++k) tot += d[k];
     const int32_t incl = wave_incl_scan(tot, lane);
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
+    mark_phase(1);
     int32_t off = carry + incl - tot, batch_total = 0;
 #pragma unroll
     for (int w = 0; w < kNatThreads / 64; ++w) {
@@ -342,6 +353,7 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
         rr[k] = live ? ((pc & 63) << 16) | r : -1;
     }
     __syncthreads();
+    mark_phase(2);
     {
         int32_t cnt = 0;
         const int32_t w_hi = min(32 * qq + 32, span_words);
@@ -358,6 +370,7 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
         qbase[t] = cnt;
     }
     __syncthreads();
+    mark_phase(3);
     if (wave == 0) {   // lane = column: quarter bases, the column scan, the list header
         int32_t q4[4], ctot = 0;
 #pragma unroll
@@ -374,6 +387,7 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
         }
     }
     __syncthreads();
+    mark_phase(4);
     uint32_t *out = lists + boff[b * 4 + g];
 #pragma unroll
     for (int k = 0; k < kNatPer; ++k) {
@@ -383,6 +397,14 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
         const int32_t slot = qbase[4 * q + (r >> 10)] + wbase[bi] + __popc(bits[bi] & ((1u << (r & 31)) - 1u));
         out[slot] = X1 ? __float_as_uint(__fmul_rn(xv[k], tab[id[k]]))
                        : (uint32_t)(r + row_lo) | ((uint32_t)id[k] << 23);
+    }
+    if constexpr (PROF) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        mark_phase(5);
+        if (t == 0) {
+            ph[7] = 1;
+            for (int k = 0; k < 8; ++k) atomicAdd(prof + k, ph[k]);
+        }
     }
 }
 
@@ -488,8 +510,32 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
                 hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
                                    nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel, nd.d_bcarry,
                                    nd.d_boff, nd.d_table, nd.table_size, a, alpha, nd.d_lists, nd.d_hdr);
-            const hipError_t e = hipGetLastError();
+            hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
+#ifdef SM_DEV
+            if (dev_env("SM_NAT_PROF")) {   // the decode again, profiled (same outputs)
+                unsigned long long *d = nullptr, h[8] = {};
+                if (hipMalloc(&d, sizeof(h)) != hipSuccess) return hipErrorOutOfMemory;
+                (void)hipMemsetAsync(d, 0, sizeof(h), s);
+                if (m == 1)
+                    hipLaunchKernelGGL((native_decode_kernel<true, true>), dgrid, dim3(kNatThreads), 0, s,
+                                       nd.d_pos, nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel,
+                                       nd.d_bcarry, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                       nd.d_lists, nd.d_hdr, d);
+                else
+                    hipLaunchKernelGGL((native_decode_kernel<false, true>), dgrid, dim3(kNatThreads), 0, s,
+                                       nd.d_pos, nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel,
+                                       nd.d_bcarry, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                       nd.d_lists, nd.d_hdr, d);
+                (void)hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                (void)hipFree(d);
+                const double w = (double)h[7];
+                fprintf(stderr, "native decode prof (kcycles per workgroup, %.0f wgs): meta+load %.2f scan %.2f "
+                        "mark %.2f rank1 %.2f rank2 %.2f place+drain %.2f\n", w, h[0] / w / 1e3, h[1] / w / 1e3,
+                        h[2] / w / 1e3, h[3] / w / 1e3, h[4] / w / 1e3, h[5] / w / 1e3);
+            }
+#endif
         }
         const dim3 agrid((unsigned)P, 256 / kNatCols, (unsigned)(m == 1 ? 1 : (m + 4 * RT - 1) / (4 * RT)));
 #define SM_NAT_APPLY(RR, XX)                                                                  \
