@@ -242,6 +242,17 @@ SM_API sm_status sm_copy_ref_stream(const sm_matrix *m, uint8_t *pos, uint8_t *v
                                     int32_t *panel_row_off, int32_t *panel_col_off,
                                     int64_t *panel_begin, int64_t *panel_end);
 
+/* The reference encoding of a matrix built from CSR (sm_create_from_csr*, or the
+ * device CopyForm scan), built on the host from its CSR by the reference's own stream
+ * rules (sparse-matrix.cc:20-99: 256-column panels, row-major, uint8 delta steps with
+ * (255, T) fillers, uint8 ids): afterwards sm_copy_ref_stream, sm_equal's member-wise
+ * comparison and SM_ALGO_NATIVE serve the matrix.  `table` (table_size <= 255 entries)
+ * is the codebook every value must match bit for bit (the first equal entry's id);
+ * NULL takes the values' distinct bit patterns in CSR order (SM_ERR_NOT_SUPPORTED past
+ * 255).  A matrix that already holds the encoding is left as it is.  Not concurrent with
+ * other calls on the matrix.  Additive: the reference cannot hold a matrix without it. */
+SM_API sm_status sm_build_ref_stream(sm_matrix *m, const float *table, int32_t table_size);
+
 /* Host copy of the device CSR (row_ptr n_rows+1, col_idx/val nnz). */
 SM_API sm_status sm_copy_csr(const sm_matrix *m, int32_t *row_ptr, int32_t *col_idx, float *val);
 

@@ -40,6 +40,7 @@ EXPORTS = (
     "sm_create_from_csr_device", "sm_build_opts_init", "sm_create_from_csr_ex",
     "sm_create_from_csr_device_ex",
     "sm_destroy", "sm_get_info", "sm_get_info_ex", "sm_num_rows", "sm_num_cols", "sm_copy_ref_stream",
+    "sm_build_ref_stream",
     "sm_copy_csr", "sm_to_dense", "sm_equal", "sm_spmv", "sm_spmm", "sm_addmatmat",
     "sm_addmatmat_host", "sm_beta_scale", "sm_transpose", "sm_panel_kernel", "sm_stream_sync",
     "sm_multi_last_error", "sm_multi_partition", "sm_multi_unique_id", "sm_multi_create",
@@ -133,6 +134,7 @@ def _declare(L):
         "sm_num_rows": ([_vp], _i32),
         "sm_num_cols": ([_vp], _i32),
         "sm_copy_ref_stream": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+        "sm_build_ref_stream": ([_vp, _vp, _i32], C.c_int),
         "sm_copy_csr": ([_vp, _vp, _vp, _vp], C.c_int),
         "sm_to_dense": ([_vp, _vp, _i32, C.c_int], C.c_int),
         "sm_equal": ([_vp, _vp], _i32),

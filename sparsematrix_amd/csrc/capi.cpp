@@ -126,8 +126,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.nat.d_col);
     (void)hipFree(m->plan.nat.d_table);
     (void)hipFree(m->plan.nat.d_pbatch);
-    (void)hipFree(m->plan.nat.d_bpanel);
-    (void)hipFree(m->plan.nat.d_bcarry);
+    (void)hipFree(m->plan.nat.d_bmeta);
     (void)hipFree(m->plan.nat.d_boff);
     (void)hipFree(m->plan.nat.d_lists);
     (void)hipFree(m->plan.nat.d_hdr);
@@ -683,16 +682,16 @@ sm_status upload_native(sm_matrix *m) {
     d.n_all = (int32_t)Pc;
     // Batch metadata of the two-kernel form: the carry before each batch and the live
     // entries of each (batch, group) -- derived from the stream once, as the panel bounds are.
-    std::vector<int32_t> pbatch(Pc + 1, 0), bpanel, bcarry, boff;
+    std::vector<int32_t> pbatch(Pc + 1, 0), boff;
+    std::vector<NatBatch> bmeta;
     int64_t live_total = 0;
     for (size_t p = 0; p < Pc; p++) {
-        pbatch[p] = (int32_t)bpanel.size();
+        pbatch[p] = (int32_t)bmeta.size();
         int32_t carry = 0;
         for (int64_t e0 = beg[p]; e0 < end[p]; e0 += kNatBatchEntries) {
-            bpanel.push_back((int32_t)p);
-            bcarry.push_back(carry);
-            int64_t live[4] = {0, 0, 0, 0};
             const int64_t e1 = std::min<int64_t>(end[p], e0 + kNatBatchEntries);
+            bmeta.push_back(NatBatch{e0, (int32_t)(e1 - e0), carry});
+            int64_t live[4] = {0, 0, 0, 0};
             for (int64_t e = e0; e < e1; e++) {
                 carry += pos[(size_t)e];
                 if (val[(size_t)e] < m->table_size) live[(carry & 255) >> 6]++;
@@ -702,21 +701,19 @@ sm_status upload_native(sm_matrix *m) {
                 live_total += live[g];
             }
         }
-        d.max_panel_batches = std::max<int32_t>(d.max_panel_batches, (int32_t)bpanel.size() - pbatch[p]);
+        d.max_panel_batches = std::max<int32_t>(d.max_panel_batches, (int32_t)bmeta.size() - pbatch[p]);
     }
-    pbatch[Pc] = (int32_t)bpanel.size();
-    d.n_batches = (int32_t)bpanel.size();
+    pbatch[Pc] = (int32_t)bmeta.size();
+    d.n_batches = (int32_t)bmeta.size();
     if (live_total >= ((int64_t)1 << 31)) return SM_OK;   // fused kernel only
     if (d.n_batches > 0 && d.max_panel_batches > kNatFusedBatches) {
         SM_TRY_HIP(dev_alloc(&d.d_pbatch, (int64_t)Pc + 1, m->device_bytes));
-        SM_TRY_HIP(dev_alloc(&d.d_bpanel, (int64_t)d.n_batches, m->device_bytes));
-        SM_TRY_HIP(dev_alloc(&d.d_bcarry, (int64_t)d.n_batches, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_bmeta, (int64_t)d.n_batches, m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_boff, (int64_t)d.n_batches * 4, m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_lists, std::max<int64_t>(live_total, 1), m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_hdr, (int64_t)d.n_batches * 256, m->device_bytes));
         SM_TRY_HIP(hipMemcpy(d.d_pbatch, pbatch.data(), (Pc + 1) * 4, hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(d.d_bpanel, bpanel.data(), bpanel.size() * 4, hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(d.d_bcarry, bcarry.data(), bcarry.size() * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_bmeta, bmeta.data(), bmeta.size() * sizeof(NatBatch), hipMemcpyHostToDevice));
         SM_TRY_HIP(hipMemcpy(d.d_boff, boff.data(), boff.size() * 4, hipMemcpyHostToDevice));
     }
     return SM_OK;
@@ -1299,6 +1296,35 @@ sm_status sm_copy_ref_stream(const sm_matrix *m, uint8_t *pos, uint8_t *val, int
     if (pb && P) memcpy(pb, m->panel_begin.data(), P * 8);
     if (pe && P) memcpy(pe, m->panel_end.data(), P * 8);
     return SM_OK;
+}
+
+sm_status sm_build_ref_stream(sm_matrix *m, const float *table, int32_t table_size) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    if (m->has_ref) return SM_OK;
+    if (table && (table_size < 0 || table_size > 255))
+        return fail(SM_ERR_INVALID_ARG, "table_size %d not in [0, 255]", table_size);
+    DeviceGuard g(m->device);
+    std::vector<int32_t> rp((size_t)m->n_rows + 1), col((size_t)m->nnz);
+    std::vector<float> val((size_t)m->nnz);
+    sm_status st = sm_copy_csr(m, rp.data(), col.data(), val.data());
+    if (st != SM_OK) return st;
+    EncodeResult er;
+    const int rc = encode_csr_ref(rp.data(), col.data(), val.data(), m->n_rows, m->n_cols, table,
+                                  table_size, er);
+    if (rc == -2) return fail(SM_ERR_INVALID_ARG, "a value is not in the codebook");
+    if (rc == -3) return fail(SM_ERR_NOT_SUPPORTED, "more than 255 distinct values: no uint8 ids");
+    if (rc == -4) return fail(SM_ERR_NOT_SUPPORTED, "S rows >= 2^23: the reference's int32 offsets overflow");
+    if (rc != 0) return fail(SM_ERR_INVALID_ARG, "bad codebook");
+    m->table_size = er.table_size;
+    m->table = std::move(er.table);
+    m->pos = std::move(er.pos);
+    m->val = std::move(er.val_id);
+    m->panel_row_off = std::move(er.panel_row_off);
+    m->panel_col_off = std::move(er.panel_col_off);
+    m->panel_begin = std::move(er.panel_begin);
+    m->panel_end = std::move(er.panel_end);
+    m->has_ref = true;
+    return upload_native(m);
 }
 
 sm_status sm_copy_csr(const sm_matrix *m, int32_t *row_ptr, int32_t *col_idx, float *val) {

@@ -10,6 +10,7 @@
 // Indexing is 64-bit (the reference's int32 `i*stride+j` overflows above ~46k^2,
 // SURVEY.md §0.4); everything else follows the reference rule for rule.
 #include <cstring>
+#include <unordered_map>
 
 #include "encode.h"
 
@@ -115,6 +116,76 @@ int encode_dense_index(const uint8_t *dm, int32_t rows, int32_t cols, int32_t st
             out.panel_begin.push_back(begin);
             out.panel_end.push_back((int64_t)out.pos.size());
         }
+    }
+    return 0;
+}
+
+int encode_csr_ref(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
+                   int64_t n_cols, const float *table, int32_t table_size, EncodeResult &out) {
+    out = EncodeResult();
+    if (n_cols >= ((int64_t)1 << (31 - kPanelShift))) return -4;
+    const int64_t nnz = n_rows > 0 ? rp[n_rows] : 0;
+    auto bits_of = [](float v) {
+        uint32_t u;
+        memcpy(&u, &v, 4);
+        return u;
+    };
+    // Codebook: value bits -> id (the first table entry with those bits, as a dense index
+    // naming either of two equal entries would decode to the same value).
+    std::unordered_map<uint32_t, uint8_t> id_of;
+    if (table) {
+        if (table_size < 0 || table_size > kMaxStep) return -1;
+        for (int32_t i = 0; i < table_size; i++) id_of.emplace(bits_of(table[i]), (uint8_t)i);
+        out.table.assign(table, table + table_size);
+    } else {
+        for (int64_t e = 0; e < nnz; e++) {
+            const uint32_t u = bits_of(val[e]);
+            if (id_of.count(u)) continue;
+            if ((int32_t)id_of.size() == kMaxStep) return -3;
+            id_of.emplace(u, (uint8_t)id_of.size());
+            out.table.push_back(val[e]);
+        }
+        table_size = (int32_t)out.table.size();
+    }
+    out.table.push_back(0.0f);
+    out.table_size = table_size;
+    out.s_rows = n_cols;
+    out.s_cols = n_rows;
+    if (table_size == 0) return nnz == 0 ? 0 : -2;
+    const uint8_t T = (uint8_t)table_size;
+    std::vector<std::pair<uint64_t, uint8_t>> ent;
+    for (int64_t c0 = 0; c0 < n_rows; c0 += kPanelW) {
+        const int64_t w = std::min<int64_t>(kPanelW, n_rows - c0);
+        ent.clear();
+        for (int64_t c = 0; c < w; c++)
+            for (int64_t e = rp[c0 + c]; e < rp[c0 + c + 1]; e++) {
+                const auto it = id_of.find(bits_of(val[e]));
+                if (it == id_of.end()) return -2;
+                ent.push_back({((uint64_t)(uint32_t)col[e] << kPanelShift) | (uint64_t)c, it->second});
+            }
+        if (ent.empty()) continue;
+        // row-major in the panel (S row, then S column), as the reference scans (:65-95)
+        std::stable_sort(ent.begin(), ent.end(),
+                         [](const std::pair<uint64_t, uint8_t> &a, const std::pair<uint64_t, uint8_t> &b) {
+                             return a.first < b.first;
+                         });
+        const int64_t begin = (int64_t)out.pos.size();
+        int64_t prev = 0;
+        for (const auto &pe : ent) {
+            int64_t gap = (int64_t)pe.first - prev;
+            while (gap > kMaxStep) {
+                out.pos.push_back((uint8_t)kMaxStep);
+                out.val_id.push_back(T);
+                gap -= kMaxStep;
+            }
+            out.pos.push_back((uint8_t)gap);
+            out.val_id.push_back(pe.second);
+            prev = (int64_t)pe.first;
+        }
+        out.panel_row_off.push_back(0);
+        out.panel_col_off.push_back((int32_t)c0);
+        out.panel_begin.push_back(begin);
+        out.panel_end.push_back((int64_t)out.pos.size());
     }
     return 0;
 }

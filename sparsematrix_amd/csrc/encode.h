@@ -23,6 +23,14 @@ struct EncodeResult {
 int encode_dense_index(const uint8_t *dm, int32_t rows, int32_t cols, int32_t stride,
                        const float *table, int32_t table_size, bool trans, EncodeResult &out);
 
+// The reference encoding of a CSR matrix of B = S^T (n_rows = S columns, n_cols = S
+// rows): the inverse of the CSR pass above, the stream rules of sparse-matrix.cc:32-95.
+// table == nullptr: the codebook is the values' distinct fp32 bit patterns in CSR order.
+// Returns 0; -1 bad table_size; -2 a value not in the table; -3 more than 255 distinct
+// values; -4 S rows >= 2^23 (the reference's int32 in-panel offsets).
+int encode_csr_ref(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
+                   int64_t n_cols, const float *table, int32_t table_size, EncodeResult &out);
+
 struct TileHost {
     int32_t r0, r1, flags;
 };

@@ -276,9 +276,7 @@ __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
 template <bool X1, bool PROF = false>
 __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
-    const int64_t *__restrict__ pbeg, const int64_t *__restrict__ pend,
-    const int32_t *__restrict__ pbatch, const int32_t *__restrict__ bpanel,
-    const int32_t *__restrict__ bcarry, const int32_t *__restrict__ boff,
+    const NatBatch *__restrict__ bmeta, const int32_t *__restrict__ boff,
     const float *__restrict__ table, int32_t T, const float *__restrict__ x, float alpha,
     uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr, unsigned long long *__restrict__ prof = nullptr) {
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -299,8 +297,9 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int qc = t >> 2, qq = t & 3;
     const int32_t b = blockIdx.x, g = blockIdx.y;
-    const int32_t p = bpanel[b];
-    const int64_t e0 = pbeg[p] + (int64_t)(b - pbatch[p]) * kNatBatch, e_end = pend[p];
+    const NatBatch bm = bmeta[b];
+    const int64_t e0 = bm.start, e_end = bm.start + bm.len;
+    const int32_t list_off = boff[b * 4 + g];
     if (X1) tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
     for (int w = t; w <= kDummyWord; w += kNatThreads) bits[w] = 0u;
     uint8_t d[kNatPer], id[kNatPer];
@@ -320,7 +319,7 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
             }
         }
     }
-    const int32_t carry = bcarry[b];
+    const int32_t carry = bm.carry;
     mark_phase(0);
     int32_t tot = 0;
 #pragma unroll
@@ -378,8 +377,10 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
             q4[q] = qbase[4 * lane + q];
             ctot += q4[q];
         }
-        int32_t cb = wave_incl_scan(ctot, lane) - ctot;
-        hdr[((int64_t)b * 4 + g) * kNatCols + lane] = (uint32_t)cb | ((uint32_t)(cb + ctot) << 16);
+        const int32_t cincl = wave_incl_scan(ctot, lane);
+        int32_t cb = cincl - ctot;
+        hdr[((int64_t)b * 4 + g) * kNatCols + lane] = (uint32_t)cb | ((uint32_t)cincl << 16);
+        if (lane == 63) wsum[0] = cincl;   // the group's live entries
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             qbase[4 * lane + q] = cb;
@@ -388,16 +389,26 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     }
     __syncthreads();
     mark_phase(4);
-    uint32_t *out = lists + boff[b * 4 + g];
+    // Slots and values in registers, then staged in LDS over the bitmap (no longer read)
+    // and written out with coalesced stores.
+    int32_t slot[kNatPer];
+    uint32_t v[kNatPer];
 #pragma unroll
     for (int k = 0; k < kNatPer; ++k) {
-        if (rr[k] < 0) continue;
-        const int32_t q = rr[k] >> 16, r = rr[k] & 0xFFFF;
-        const int32_t bi = bit_index(q, r >> 5);
-        const int32_t slot = qbase[4 * q + (r >> 10)] + wbase[bi] + __popc(bits[bi] & ((1u << (r & 31)) - 1u));
-        out[slot] = X1 ? __float_as_uint(__fmul_rn(xv[k], tab[id[k]]))
-                       : (uint32_t)(r + row_lo) | ((uint32_t)id[k] << 23);
+        const bool live = rr[k] >= 0;
+        const int32_t q = live ? rr[k] >> 16 : 0, r = live ? rr[k] & 0xFFFF : 0;
+        const int32_t bi = live ? bit_index(q, r >> 5) : kDummyWord;
+        slot[k] = live ? qbase[4 * q + (r >> 10)] + wbase[bi] + __popc(bits[bi] & ((1u << (r & 31)) - 1u)) : -1;
+        v[k] = X1 ? __float_as_uint(__fmul_rn(xv[k], tab[id[k]])) : (uint32_t)(r + row_lo) | ((uint32_t)id[k] << 23);
     }
+    const int32_t n_live = wsum[0];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kNatPer; ++k)
+        if (slot[k] >= 0) bits[slot[k]] = v[k];
+    __syncthreads();
+    uint32_t *out = lists + list_off;
+    for (int32_t i = t; i < n_live; i += kNatThreads) out[i] = bits[i];
     if constexpr (PROF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         mark_phase(5);
@@ -504,12 +515,12 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
             const dim3 dgrid((unsigned)nd.n_batches, 256 / kNatCols);
             if (m == 1)
                 hipLaunchKernelGGL(native_decode_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
-                                   nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel, nd.d_bcarry,
-                                   nd.d_boff, nd.d_table, nd.table_size, a, alpha, nd.d_lists, nd.d_hdr);
+                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                   nd.d_lists, nd.d_hdr);
             else
                 hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
-                                   nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel, nd.d_bcarry,
-                                   nd.d_boff, nd.d_table, nd.table_size, a, alpha, nd.d_lists, nd.d_hdr);
+                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                   nd.d_lists, nd.d_hdr);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
 #ifdef SM_DEV
@@ -519,14 +530,12 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
                 (void)hipMemsetAsync(d, 0, sizeof(h), s);
                 if (m == 1)
                     hipLaunchKernelGGL((native_decode_kernel<true, true>), dgrid, dim3(kNatThreads), 0, s,
-                                       nd.d_pos, nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel,
-                                       nd.d_bcarry, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
-                                       nd.d_lists, nd.d_hdr, d);
+                                       nd.d_pos, nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table,
+                                       nd.table_size, a, alpha, nd.d_lists, nd.d_hdr, d);
                 else
                     hipLaunchKernelGGL((native_decode_kernel<false, true>), dgrid, dim3(kNatThreads), 0, s,
-                                       nd.d_pos, nd.d_val, nd.d_beg, nd.d_end, nd.d_pbatch, nd.d_bpanel,
-                                       nd.d_bcarry, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
-                                       nd.d_lists, nd.d_hdr, d);
+                                       nd.d_pos, nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table,
+                                       nd.table_size, a, alpha, nd.d_lists, nd.d_hdr, d);
                 (void)hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
                 (void)hipStreamSynchronize(s);
                 (void)hipFree(d);

@@ -124,6 +124,12 @@ struct CcsellDev {
 
 // Device copy of the reference's own stream (native.hip): uint8 deltas + ids, each
 // panel's run starting 16-byte aligned (padded with zero-delta fillers).
+struct NatBatch {   // one batch of the native two-kernel form (16 bytes, one load)
+    int64_t start;     // first entry in the padded stream
+    int32_t len;       // entries (<= kNatBatchEntries)
+    int32_t carry;     // in-panel offset before the batch (kernel.cc:780-781)
+};
+
 struct NativeDev {
     int32_t n_panels = 0;             // panels with entries; 0 when not built
     int32_t n_all = 0;                // + the empty 256-column blocks (beta != 1 launches)
@@ -140,7 +146,7 @@ struct NativeDev {
     // the list's [begin, end) written by the decode kernel.
     int32_t n_batches = 0, max_panel_batches = 0;
     int32_t *d_pbatch = nullptr;      // n_all + 1: first batch of each panel
-    int32_t *d_bpanel = nullptr, *d_bcarry = nullptr;   // per batch
+    NatBatch *d_bmeta = nullptr;      // per batch: stream start, entries, carry
     int32_t *d_boff = nullptr;        // per (batch, group)
     uint32_t *d_lists = nullptr;      // live entries: m = 1 the term's bits, else row | id << 23
     uint32_t *d_hdr = nullptr;        // per (batch, group, column): begin | end << 16

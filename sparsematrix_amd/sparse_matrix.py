@@ -220,6 +220,17 @@ class SparseMatrix:
         check(self._L.sm_copy_csr(self._h, _ptr(rp), _ptr(ci), _ptr(va)), "sm_copy_csr")
         return rp, ci[: inf["nnz"]], va[: inf["nnz"]]
 
+    def build_ref_stream(self, table: Optional[np.ndarray] = None) -> None:
+        """Encode a CSR-built matrix in the reference's format (sm_build_ref_stream,
+        sparse-matrix.cc:20-99): afterwards ref_stream(), == and algo="native" serve it.
+        `table`: the codebook (<= 255 fp32 values every value must match); None takes the
+        values' distinct bit patterns in CSR order."""
+        if table is None:
+            check(self._L.sm_build_ref_stream(self._h, None, 0), "sm_build_ref_stream")
+            return
+        tb = np.ascontiguousarray(table, np.float32)
+        check(self._L.sm_build_ref_stream(self._h, _ptr(tb), int(tb.size)), "sm_build_ref_stream")
+
     def ref_stream(self) -> dict:
         """The reference encoding (pos_index_, val_index_, block bounds)."""
         inf = self.info()

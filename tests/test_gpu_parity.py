@@ -826,6 +826,67 @@ def test_golden_addmatmat_native(sm, name):
         assert bits_equal(to_host(y), r.out.reshape(r.m, r.ldc)[0, :n])
 
 
+@pytest.mark.parametrize("name", case_names())
+def test_golden_csr_to_reference_stream(sm, name):
+    """CSR -> reference stream (sm_build_ref_stream, sparse-matrix.cc:20-99): the matrix
+    rebuilt from its own CSR and encoded with the case's table holds the compiled
+    reference's stream, panels and table exactly (so == is member-wise true), and
+    AddMatMat straight from that stream (SM_ALGO_NATIVE) gives the reference's outputs."""
+    c = load_case(name)
+    M = _from_case(sm, c)
+    rp, ci, va = M.csr()
+    R = sm.SparseMatrix.from_csr(rp, ci, va, c.s_rows)
+    assert R.info()["has_ref_stream"] == 0
+    R.build_ref_stream(c.table[: c.table_size] if c.table_size else None)
+    st = R.ref_stream()
+    assert st["rows"] == c.s_rows and st["cols"] == c.s_cols
+    assert np.array_equal(st["pos"], c.pos)
+    assert np.array_equal(st["panel_col_off"], c.panel_col_off)
+    assert np.array_equal(st["panel_begin"], c.panel_begin)
+    assert np.array_equal(st["panel_end"], c.panel_end)
+    tb = np.concatenate([c.table[: c.table_size], np.zeros(1, np.float32)]).view(np.uint32)
+    if np.unique(tb[: c.table_size]).size == c.table_size:
+        assert np.array_equal(st["val"], c.val) and R == M   # ids are unambiguous
+    else:   # equal table entries: the first id is named, the decoded bits agree
+        assert np.array_equal(tb[st["val"]], tb[c.val])
+    for r in c.runs[:3]:
+        c_d = to_dev(r.c)
+        R.AddMatMat(to_dev(r.a), r.m, r.lda, c_d, r.ldc, r.alpha, r.beta, algo="native")
+        assert bits_equal(to_host(c_d), r.out), (r.m, r.alpha, r.beta)
+
+
+def test_csr_to_reference_stream_device_built(sm):
+    """A matrix ingested from device CSR (no dense index anywhere) gets the reference
+    encoding with a derived codebook: its stream decodes (oracle.RefModel over the
+    equivalent dense index) to the same AddMatMat, bit for bit; > 255 distinct values
+    decline with SM_ERR_NOT_SUPPORTED, values outside a given table with INVALID_ARG."""
+    torch = torch_dev()
+    rng = np.random.default_rng(12)
+    k, n, m = 700, 900, 3
+    table = rng.uniform(-1, 1, 40).astype(np.float32)
+    dm = np.where(rng.random((n, k)) < 0.03, rng.integers(0, 40, (n, k)), 255).astype(np.uint8)
+    M = sm.SparseMatrix(dm, n, k, k, table, 40, sm.SblasTrans)
+    rp, ci, va = M.csr()
+    R = sm.SparseMatrix.from_csr(torch.from_numpy(rp).cuda(), torch.from_numpy(ci).cuda(),
+                                 torch.from_numpy(va).cuda(), k)
+    R.build_ref_stream()
+    assert R.info()["has_ref_stream"] == 1
+    ref = oracle.RefModel(dm, n, k, k, table, 40, trans=True)
+    A = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+    C = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+    want = ref.add_mat_mat(A.reshape(-1), m, k, C.reshape(-1), n, 1.3, 0.7)
+    c_d = to_dev(C.reshape(-1))
+    R.AddMatMat(to_dev(A.reshape(-1)), m, k, c_d, n, 1.3, 0.7, algo="native")
+    assert bits_equal(to_host(c_d), want)
+    W = sm.SparseMatrix.from_csr(np.array([0, 300], np.int32), np.arange(300, dtype=np.int32),
+                                 np.arange(300, dtype=np.float32), 300)
+    with pytest.raises(sm.SparseMatrixError):
+        W.build_ref_stream()
+    with pytest.raises(sm.SparseMatrixError):
+        R2 = sm.SparseMatrix.from_csr(rp, ci, va, k)
+        R2.build_ref_stream(table[:10])
+
+
 def test_native_beta_scales_columns_without_panels(sm):
     """Column blocks with no entries have no panel in the reference stream, yet beta
     scales all of C (sparse-matrix.cc:149-151): the native launch covers them too."""

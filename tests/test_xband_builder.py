@@ -71,3 +71,21 @@ def test_ccsell_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ccsell_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_encode_csr_ref_under_asan(tmp_path):
+    """CSR -> reference-stream converter (encode.cpp encode_csr_ref, behind
+    sm_build_ref_stream): the dense encoder's CSR converted back gives its stream, panels
+    and table exactly (the dense encoder is pinned to the compiled reference by the golden
+    fixtures); a derived codebook decodes to the same values; bad inputs decline."""
+    exe = tmp_path / "encode_csr_asan"
+    src = [os.path.join(ROOT, "tests", "native", "encode_csr_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "encode.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "encode_csr_asan: ok" in r.stdout
