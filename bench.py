@@ -530,7 +530,7 @@ def main():
 
 def cpu_baseline(args, r0, bytes_rank, rmat_host):
     """B2 (same-order CSR, all cores + 1 thread), B1 (the reference-format
-    twin, 1 thread, config 1 and 16k^2), B2 on R-MAT.  The oracle is the checker and
+    twin, 1 thread, config 1 and 16k^2), B3 (dense sgemv, config 1), B2 on R-MAT.  The oracle is the checker and
     this CPU baseline only; nothing of it runs in the timed GPU region."""
     import oracle
     from sparsematrix_amd import synth
@@ -591,6 +591,26 @@ def cpu_baseline(args, r0, bytes_rank, rmat_host):
         "kind": "port", "cores": 1, "cases": b1,
         "sample": "oracle/refmodel.c AddMatMat on the reference's own format (m = 1, alpha 1, "
                   "beta 0.5), B = dense uint8 id matrix (Trans), codebook of 255 floats"}
+    # B3: the dense baseline of the reference's harness (cblas_sgemv/sgemm on the dense
+    # matrix, blas_test.h), config 1 only, through numpy's bundled OpenBLAS -- the only
+    # OpenBLAS on the box (the reference's vendored "plus" builds are ARM-only).
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+        blas = [i for i in threadpool_info() if i.get("user_api") == "blas"]
+        rng = np.random.default_rng(1)
+        dense = np.where(rng.random((1024, 1024)) < 0.01,
+                         rng.uniform(-1, 1, (1024, 1024)), 0.0).astype(np.float32)
+        xv = rng.uniform(-1, 1, 1024).astype(np.float32)
+        yv = rng.uniform(-1, 1, 1024).astype(np.float32)
+        with threadpool_limits(limits=1, user_api="blas"):
+            k, t_r = timed(lambda: 0.5 * yv + dense @ xv, min(2.0, sec / 4))
+        out["b3_dense_sgemv_config1_1thread"] = {
+            "ms": round(1e3 * t_r / k, 4), "reps": k, "cores": 1,
+            "blas": (blas[0].get("internal_api", "?") + " " + str(blas[0].get("version", "")))
+            if blas else "unknown",
+            "sample": "y = 0.5 y + A x, A the dense 1024 x 1024 fp32 matrix (1 % nonzero), numpy's BLAS"}
+    except Exception as exc:  # noqa: BLE001
+        out["b3_dense_sgemv_config1_1thread"] = {"unavailable": f"{type(exc).__name__}: {exc}"[:200]}
     if rmat_host is not None:
         rrp, rci, rva, rx, ry, rb = rmat_host
         k, t_r = timed(lambda: oracle.csr_spmv_mt(rrp, rci, rva, rx, ry, 1.0, 0.5, threads=threads),
