@@ -266,8 +266,28 @@ XbKind xband_kind_setting(const sm_matrix *m) {
 }
 
 // Sweeping x through LDS (or walking its bands) pays when the L2 -> LDS bytes of
-// one kind's row blocks stay within 20x the matrix stream.
+// one kind's row blocks stay within 20x the matrix stream.  The gather kind sweeps no
+// x: its cost is its bands' skeleton plus its terms, set against the sliced ELL's cost
+// per term on wide uniform matrices -- constants from the two measured wide shapes
+// (config 2 rows at 8M columns: 16K bands of 1K terms, 93 us; config 5's rank slice,
+// 8M x 64M: 1M bands of 128 terms, 1.60 ms; its ccsell 2.30 ms = 17 ps per term).
+static bool gather_cost_ok(const sm_matrix *m) {
+    // Calibrated on uniform rows: skewed ones (longest row > 64x the mean, e.g. R-MAT)
+    // keep the sliced ELL, whose long-row segments balance them.
+    if ((double)m->plan.max_row_nnz > 64.0 * (double)m->nnz / (double)std::max<int64_t>(1, m->n_rows))
+        return false;
+    const int64_t nblk = (m->n_rows + (1 << kXbGatherRowsLog2) - 1) >> kXbGatherRowsLog2;
+    const double bands = (double)nblk * (double)((m->n_cols + (1 << kXbGatherWideBandLog2) - 1) >>
+                                                 kXbGatherWideBandLog2);
+    const double per_band_us = 0.25 + 1.2e-3 * (double)m->nnz / bands;
+    const double gather_us = bands / 256.0 * per_band_us;
+    const double sell_us = 1.7e-5 * (double)m->nnz;
+    return gather_us < sell_us;
+}
+
 static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
+    if (kind == kXbGather && m->n_cols > kGatherCols && m->opts.gather_band_log2 == 0)
+        return gather_cost_ok(m);
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
                           : kind == kXbBand2 || kind == kXbCband ? kB2RowBits
                           : kind == kXbGather ? kXbGatherRowsLog2
