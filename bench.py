@@ -110,10 +110,14 @@ KERNELS = {"stream": "spmv_stream_kernel",
            "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)",
            "band2": "spmv_band2_kernel (balanced bands, distributed slab combine)",
            "cband": "spmv_band2_kernel<CB> (balanced bands of 4-byte codebook words, "
-                    "distributed slab combine)"}
+                    "distributed slab combine)",
+           "ccsell": "spmv_ccsell_kernel (column-chunked sorted sliced-ELL)",
+           "sweep": "spmv_sweep_kernel (column-swept 256-row blocks, one wavefront each)"}
 
 
 def layout_of(info: dict) -> str:
+    if info.get("sweep_blocks"):
+        return "sweep"
     if info["has_xband"]:
         return LAYOUTS[info["has_xband"]]
     if info.get("ccsell_chunks"):

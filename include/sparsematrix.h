@@ -122,7 +122,8 @@ typedef struct sm_info {
                                    it serves SpMV when built (AUTO, SELL): every row bit-identical */
     int32_t hot_cols;           /* > 0: the relabeled columns [0, hot_cols) run as codebook bands
                                    before the sliced ELL adds the other terms (AUTO, SELL)  */
-    int32_t reserved1;
+    int32_t sweep_blocks;       /* row blocks of the column-swept layout (0: not built); it
+                                   serves SpMV when built (AUTO): every row bit-identical    */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -185,8 +186,10 @@ typedef enum sm_layout {
     SM_LAYOUT_BAND2 = 4,     /* balanced bands, 8-byte entries                             */
     SM_LAYOUT_CBAND = 5,     /* balanced bands, 4-byte codebook words                      */
     SM_LAYOUT_NO_BANDS = 6,  /* no band layout: sorted sliced-ELL, else the stream kernel   */
-    SM_LAYOUT_BANDS = 7      /* a band layout even where the cost model would decline; the
+    SM_LAYOUT_BANDS = 7,     /* a band layout even where the cost model would decline; the
                                 kind as AUTO would pick it                                */
+    SM_LAYOUT_SWEEP = 8      /* column-swept row blocks (wide matrices, <= 255 values): one
+                                wavefront per 256 rows, terms in column order, no barrier  */
 } sm_layout;
 
 typedef struct sm_build_opts {

@@ -65,13 +65,13 @@ class SmInfo(C.Structure):
         ("xband_bands", C.c_int32), ("xband_slabs", C.c_int32), ("xband_block_rows", C.c_int32),
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
         ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("ccsell_chunks", C.c_int32),
-        ("hot_cols", C.c_int32), ("reserved1", C.c_int32),
+        ("hot_cols", C.c_int32), ("sweep_blocks", C.c_int32),
     ]
 
 
 # sm_layout
 LAYOUTS = {"auto": 0, "exact": 1, "blocked": 2, "gather": 3, "band2": 4, "cband": 5,
-           "no_bands": 6, "bands": 7}
+           "no_bands": 6, "bands": 7, "sweep": 8}
 
 
 class SmBuildOpts(C.Structure):

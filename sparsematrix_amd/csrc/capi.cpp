@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "ccsell.h"
+#include "sweep.h"
 #include "encode.h"
 #include "sm_internal.h"
 #include "sell.h"
@@ -125,6 +126,9 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.nat.d_end);
     (void)hipFree(m->plan.nat.d_col);
     (void)hipFree(m->plan.nat.d_table);
+    (void)hipFree(m->plan.sw.d_block_chunk);
+    (void)hipFree(m->plan.sw.d_ent);
+    (void)hipFree(m->plan.sw.d_table);
     (void)hipFree(m->plan.nat.d_pbatch);
     (void)hipFree(m->plan.nat.d_bmeta);
     (void)hipFree(m->plan.nat.d_boff);
@@ -190,6 +194,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         static const char *names[] = {"", "exact", "blocked", "gather", "band2", "cband"};
         for (int k = 1; k <= 5; ++k)
             if (strcmp(e, names[k]) == 0) r.layout = k;
+        if (strcmp(e, "sweep") == 0) r.layout = SM_LAYOUT_SWEEP;
     }
     if (const char *e = dev_env("SM_BAND_TALL")) r.band_tall = atoi(e);
     if (const char *e = dev_env("SM_BAND2_SLABS")) r.band_slabs = atoi(e);
@@ -213,7 +218,7 @@ sm_status check_opts(const sm_build_opts *o) {
         return fail(SM_ERR_INVALID_ARG, "sm_build_opts.struct_size %d: call sm_build_opts_init",
                     o->struct_size);
     const BuildOpts r = resolve_opts(o);
-    if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_BANDS)
+    if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_SWEEP)
         return fail(SM_ERR_INVALID_ARG, "unknown layout %d", r.layout);
     if (r.band_slabs < 0 || r.band_slabs > 16) return fail(SM_ERR_INVALID_ARG, "band_slabs not in [0, 16]");
     if (r.gather_band_log2 != 0 && (r.gather_band_log2 < 13 || r.gather_band_log2 > 15))
@@ -300,7 +305,7 @@ static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
 
 bool want_xband(const sm_matrix *m) {
     const int32_t L = m->opts.layout;
-    if (L == SM_LAYOUT_NO_BANDS) return false;
+    if (L == SM_LAYOUT_NO_BANDS || L == SM_LAYOUT_SWEEP) return false;
     if (m->nnz == 0 || m->n_rows == 0) return false;
     if (L != SM_LAYOUT_AUTO) return true;   // a forced kind, or SM_LAYOUT_BANDS
     return xband_cost_ok(m, xband_kind_setting(m));
@@ -518,7 +523,8 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
 // reference's order (the stream kernel: rows up to 64).
 bool want_sell(const sm_matrix *m) {
     if (m->opts.sell == 0) return false;
-    return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0 && m->plan.cc.n_slices == 0;
+    return m->nnz > 0 && m->n_rows > 0 && m->plan.xb.n_blocks == 0 && m->plan.cc.n_slices == 0 &&
+           m->plan.sw.n_blocks == 0;
 }
 
 sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
@@ -598,9 +604,39 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
 // the matrix -- a row-ordered ELL would gather every term's x from the Infinity Cache
 // or HBM.  It declines (and the sliced ELL serves) when one row has more than 2048
 // terms inside one column chunk.  ccsell = 0 / 1 never / always tries it.
+// Column-swept row blocks (sweep.h, kernels_sweep.hip): forced by SM_LAYOUT_SWEEP.
+bool want_sweep(const sm_matrix *m) {
+    if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0) return false;
+    return m->opts.layout == SM_LAYOUT_SWEEP;
+}
+
+sm_status upload_sweep(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    if (!codebook_ids(val, m->nnz, table, ids) || table.size() > 255) return SM_OK;   // not applicable
+    SweepHost h;
+    if (!sweep_build(rp, col, ids.data(), m->n_rows, h)) return SM_OK;
+    std::vector<uint8_t>().swap(ids);
+    SweepDev &d = m->plan.sw;
+    SM_TRY_HIP(dev_alloc(&d.d_block_chunk, (int64_t)h.block_chunk.size(), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_ent, std::max<int64_t>(1, h.n_chunks * 128), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
+    SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
+    if (!table.empty())
+        SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(d.d_block_chunk, h.block_chunk.data(), h.block_chunk.size() * 8, hipMemcpyHostToDevice));
+    if (h.n_chunks)
+        SM_TRY_HIP(hipMemcpy(d.d_ent, h.ent.data(), h.ent.size() * 4, hipMemcpyHostToDevice));
+    d.table_size = (int32_t)table.size();
+    d.n_chunks = h.n_chunks;
+    d.n_blocks = h.n_blocks;
+    return SM_OK;
+}
+
 bool want_ccsell(const sm_matrix *m) {
     if (m->opts.ccsell == 0 || m->opts.sell == 0) return false;
-    if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0 || m->plan.n_relabel > 0)
+    if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0 || m->plan.n_relabel > 0 ||
+        m->plan.sw.n_blocks > 0)
         return false;
     return m->opts.ccsell == 1 || m->n_cols >= ((int64_t)1 << 23);
 }
@@ -878,6 +914,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     }
     sm_status st2 = upload_plan(m, rp);
     if (st2 == SM_OK && want_xband(m)) st2 = upload_xband(m, rp, col, val, xband_kind_setting(m));
+    if (st2 == SM_OK && want_sweep(m)) st2 = upload_sweep(m, rp, col, val);
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     if (st2 == SM_OK && want_ccsell(m)) st2 = upload_ccsell(m, rp, col, val);
     if (st2 == SM_OK && want_sell(m)) st2 = upload_sell_layouts(m, rp, col, val);
@@ -1233,7 +1270,7 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
     // The band / sell builders run on the host (band2.cpp, xband.cpp, sell.cpp): the
     // columns come down for any of them, the values only for the layout that stores
     // them (4 + 4 bytes per term over PCIe once, at creation).
-    if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell)) {
+    if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell || want_sweep(m.get()))) {
         std::vector<int32_t> ch((size_t)nnz);
         std::vector<float> vh;
         auto values = [&]() -> sm_status {
@@ -1247,6 +1284,8 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
         st = e3 == hipSuccess ? SM_OK : hip_fail(e3, "copy CSR columns for the layout builder");
         if (st == SM_OK && xband) st = values();
         if (st == SM_OK && xband) st = upload_xband(m.get(), rp.data(), ch.data(), vh.data(), xband_kind_setting(m.get()));
+        if (st == SM_OK && want_sweep(m.get())) st = values();
+        if (st == SM_OK && want_sweep(m.get())) st = upload_sweep(m.get(), rp.data(), ch.data(), vh.data());
         if (st == SM_OK && want_relabel_size(m.get())) st = upload_relabel(m.get(), ch.data());
         if (st == SM_OK && want_ccsell(m.get())) st = values();
         if (st == SM_OK && want_ccsell(m.get())) st = upload_ccsell(m.get(), rp.data(), ch.data(), vh.data());
@@ -1296,6 +1335,7 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->sell_codebook = m->plan.sell.d_table != nullptr || m->plan.cc.d_table != nullptr;
     info->ccsell_chunks = m->plan.cc.n_slices > 0 ? m->plan.cc.n_chunks : 0;
     info->hot_cols = m->plan.hot.n_blocks > 0 ? m->plan.hot_cols : 0;
+    info->sweep_blocks = (int32_t)std::min<int64_t>(m->plan.sw.n_blocks, INT32_MAX);
     // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
     memcpy(out, &full, std::min(info_bytes, sizeof(full)));
     return SM_OK;
@@ -1459,6 +1499,10 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         break;
     case SM_ALGO_AUTO:
     case SM_ALGO_XBAND:
+        if (m->plan.sw.n_blocks > 0) {   // column-swept row blocks: no scratch, bit-identical
+            e = launch_spmv_sweep(m->plan.sw, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
+            break;
+        }
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
             e = m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
                     ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)

@@ -154,11 +154,20 @@ struct NativeDev {
 constexpr int kNatBatchEntries = 4096;
 constexpr int kNatFusedBatches = 2;   // panels of at most this many batches: one fused kernel
 
+struct SweepDev {   // column-swept row blocks (sweep.h)
+    int64_t n_blocks = 0, n_chunks = 0;   // n_blocks == 0 when not built
+    int64_t *d_block_chunk = nullptr;
+    uint32_t *d_ent = nullptr;           // n_chunks * 128
+    float *d_table = nullptr;            // 256 raw values (0 past table_size)
+    int32_t table_size = 0;
+};
+
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
     CcsellDev cc;                     // n_slices == 0 when not built
     NativeDev nat;                    // n_panels == 0 when not built (dense-index matrices)
+    SweepDev sw;                      // n_blocks == 0 when not built
     // Skewed graphs: the hottest relabeled columns [0, hot_cols) as codebook bands (x in
     // LDS), the sell layout holding only the other terms.
     XbandDev hot;                     // n_blocks == 0 when not built
@@ -198,6 +207,8 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
 hipError_t launch_long_finalize(int32_t n_long, const int32_t *long_rows, const int32_t *long_ptr,
                                 const float *partials, float *y, float beta, hipStream_t s);
 // Column-chunked sorted sliced-ELL (kernels_ccsell.hip): one launch per column chunk.
+hipError_t launch_spmv_sweep(const SweepDev &sd, int32_t n_rows, int32_t n_cols, const float *x,
+                             float *y, float alpha, float beta, hipStream_t s);
 hipError_t launch_spmv_ccsell(const CcsellDev &cd, const float *x, float *y, float alpha,
                               float beta, hipStream_t s);
 // AddMatMat on the reference's stream (native.hip): C = alpha * A * S + beta * C.

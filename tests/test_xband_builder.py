@@ -89,3 +89,20 @@ def test_encode_csr_ref_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "encode_csr_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_sweep_builder_under_asan(tmp_path):
+    """Column-swept row-block builder (sweep.cpp): each block's chunks, walked in order,
+    give every row's terms once in ascending column order with their ids; segments are
+    contiguous with continuation bits; padding is dummy; unsorted rows decline."""
+    exe = tmp_path / "sweep_asan"
+    src = [os.path.join(ROOT, "tests", "native", "sweep_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "sweep.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sweep_asan: ok" in r.stdout
