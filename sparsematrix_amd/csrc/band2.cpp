@@ -35,12 +35,17 @@ struct Seg {
 };
 
 // Lanes inside a chunk: segments of 2+ terms take consecutive lanes first (the
-// kernel passes a running sum up the lanes), then each single term of row r goes
-// to lane r mod 32 or 32 + r mod 32 when free -- so the 32 lanes of each half
-// read and write their accumulators in 32 distinct LDS banks -- else the highest
-// free lane.  cband (ids != nullptr): lane 0 is the header (the chunk's base row),
-// terms take lanes 1..63 and carry their id, row - base and a continuation flag
-// instead of value bits and rank.
+// kernel passes a running sum up the lanes), then the single terms go to the two
+// half-waves so that each half's LDS reads spread over the 32 banks: a ds_read_b32
+// is served per 32-lane half, one LDS cycle per distinct address on its busiest bank,
+// and every lane reads x[column - clo] (bank = column - clo mod 32) and the
+// accumulator of its row (bank = row mod 32).  Each single goes to the half where its
+// two banks are least used so far (ties: the emptier half), singles with the most
+// contended banks first; lane order inside a half does not matter.  Which rows share
+// a chunk and the per-row term order are unchanged (only lanes move).  cband
+// (ids != nullptr): lane 0 is the header (the chunk's base row), terms take lanes
+// 1..63 and carry their id, row - base and a continuation flag instead of value bits
+// and rank.
 void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const int32_t *col,
                 const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom) {
     bool used[64] = {false};
@@ -48,12 +53,21 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
     const bool cb = ids != nullptr;
     const int32_t base = segs.empty() ? 0 : segs.front().rl;   // segments come in row order
     int next = 0;
+    // Bank use per half: x reads (column bank) and accumulator reads (row bank).
+    uint8_t xb[2][32] = {}, yb[2][32] = {};
+    // A segment's lanes read one accumulator (a broadcast): its row counts once per half.
+    auto note = [&](int lane, uint32_t cbits, int32_t rl, bool same_row_before) {
+        const int h = lane >> 5;
+        xb[h][cbits & 31]++;
+        if (!(same_row_before && ((lane - 1) >> 5) == h)) yb[h][rl & 31]++;
+    };
     if (cb) {
         const uint32_t h = ((uint32_t)base & ((1u << kCbColBits) - 1u)) | (kCbDummyId << kCbColBits) |
                            ((((uint32_t)base >> kCbColBits) & kCbOffMask) << kCbOffShift);
         band_ent[(size_t)(wave * 64) * 2 + k] = h ^ kCbDummyWord;
         used[0] = true;
         next = 1;
+        note(0, h & ((1u << kCbColBits) - 1u), base + (int32_t)((h >> kCbOffShift) & kCbOffMask), false);
     }
     auto put = [&](const Seg &g, int32_t j, int lane) {
         const uint32_t cbits = (uint32_t)(col[g.s + j] - clo_al);
@@ -71,17 +85,53 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
             e[2 + k] = vb;
         }
         used[lane] = true;
+        note(lane, cbits, g.rl, j > 0);
     };
     for (const Seg &g : segs)
         if (g.n > 1)
             for (int32_t j = 0; j < g.n; j++) put(g, j, next++);
-    for (const Seg &g : segs) {
-        if (g.n != 1) continue;
-        const int bank = g.rl & 31;
-        int lane = !used[bank] ? bank : !used[32 + bank] ? 32 + bank : -1;
-        if (lane < 0)
-            for (lane = 63; used[lane]; lane--) {}
-        put(g, 0, lane);
+    // Singles: greedy, most contended banks first (pairwise swaps afterwards measured
+    // 2.65 / 2.44 vs 2.70 / 2.48 cycles per half-wave read, tools/band2_banks.cpp: not kept).
+    std::vector<const Seg *> single;
+    for (const Seg &g : segs)
+        if (g.n == 1) single.push_back(&g);
+    const int ns = (int)single.size();
+    if (ns == 0) return;
+    uint8_t xcnt[32] = {}, ycnt[32] = {};
+    std::vector<uint8_t> sx((size_t)ns), sy((size_t)ns), half((size_t)ns);
+    for (int i = 0; i < ns; i++) {
+        sx[(size_t)i] = (uint8_t)((col[single[(size_t)i]->s] - clo_al) & 31);
+        sy[(size_t)i] = (uint8_t)(single[(size_t)i]->rl & 31);
+        xcnt[sx[(size_t)i]]++;
+        ycnt[sy[(size_t)i]]++;
+    }
+    std::vector<int> order((size_t)ns);
+    for (int i = 0; i < ns; i++) order[(size_t)i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return xcnt[sx[(size_t)a]] + ycnt[sy[(size_t)a]] > xcnt[sx[(size_t)b]] + ycnt[sy[(size_t)b]];
+    });
+    int free_in[2] = {0, 0};
+    for (int l = 0; l < 64; l++)
+        if (!used[l]) free_in[l >> 5]++;
+    for (int i : order) {
+        int best = -1, bcost = 1 << 30;
+        for (int h = 0; h < 2; h++) {
+            if (free_in[h] == 0) continue;
+            const int a = xb[h][sx[(size_t)i]] + 1, b = yb[h][sy[(size_t)i]] + 1;
+            const int cost = 64 * (a * a + b * b) - free_in[h];
+            if (cost < bcost) { bcost = cost; best = h; }
+        }
+        half[(size_t)i] = (uint8_t)best;
+        free_in[best]--;
+        xb[best][sx[(size_t)i]]++;
+        yb[best][sy[(size_t)i]]++;
+    }
+    int lane_next[2] = {31, 63};
+    for (int i = 0; i < ns; i++) {
+        const int h = half[(size_t)i];
+        int &lane = lane_next[h];
+        while (used[lane]) lane--;
+        put(*single[(size_t)i], 0, lane);
     }
 }
 

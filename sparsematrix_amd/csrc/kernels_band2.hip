@@ -80,6 +80,12 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_E_EARLY
 #define SM_E_EARLY 0
 #endif
+#ifndef SM_CB_RFIRST
+#define SM_CB_RFIRST 0
+#endif
+#ifndef SM_CB_PIPE
+#define SM_CB_PIPE 0
+#endif
 #ifndef SM_X_AUX
 #define SM_X_AUX 0
 #endif
@@ -132,6 +138,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
     // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
     constexpr bool kEarly = SM_E_EARLY != 0;
+    // SM_CB_RFIRST (development A/B, wide cband): the apply's LDS reads go out before
+    // the next x window's LDS stores.
+    constexpr bool kRFirst = CB && !TALL && !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
+    constexpr bool kPipe = CB && !TALL && !kDma && !kEarly && SM_CB_PIPE != 0 && (ABL & ~3072) == 0;
     constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
     constexpr int U0 = AX > ER ? AX : ER;
     constexpr int U = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
@@ -325,25 +335,37 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // cband: row = chunk base (lane 0's header) + offset.  A segment's running sum
     // moves up one lane per round in lane (= column) order; the lanes a round updates
     // are an SGPR mask: the continuations whose predecessor finished last round.
-    auto apply_cb = [&](const float *xb, u32x2 e) {
-        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
-        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
+    // cband apply in two steps: cb_read decodes the chunk words and issues the six LDS
+    // reads, cb_finish adds and writes; the loop may put the next x window's LDS stores
+    // between them (SM_CB_RFIRST) so the reads do not queue behind 16 waves' stores.
+    struct CbState {
         float xv[2], yv[2], tv[2];
         uint32_t rl[2];
         uint64_t live[2], cont[2];
+    };
+    auto cb_read = [&](const float *xb, u32x2 e) -> CbState {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
+        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
+        CbState st;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
             const uint32_t base = (h & kColMask) | (((h >> kCbOffShift) & kCbOffMask) << kCbColBits);
             const uint32_t id = (wd[k] >> kCbColBits) & kCbDummyId;
-            live[k] = __ballot(id != kCbDummyId);
-            cont[k] = __ballot((int32_t)wd[k] < 0);
-            rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
-            xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd[k] & kColMask)];
-            tv[k] = (ABL & 32) ? __uint_as_float(id) : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
-            yv[k] = yacc[rl[k]];
+            st.live[k] = __ballot(id != kCbDummyId);
+            st.cont[k] = __ballot((int32_t)wd[k] < 0);
+            st.rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
+            st.xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd[k] & kColMask)];
+            st.tv[k] = (ABL & 32) ? __uint_as_float(id) : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+            st.yv[k] = yacc[st.rl[k]];
         }
+        return st;
+    };
+    auto cb_finish = [&](CbState st) {
+        float *xv = st.xv, *yv = st.yv, *tv = st.tv;
+        uint32_t *rl = st.rl;
+        uint64_t *live = st.live, *cont = st.cont;
         // Materialise all six reads before any write (one LDS wait per band).
         asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
         float tm[2], acc[2];
@@ -367,6 +389,46 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if ((last >> lane) & 1) yacc[rl[k]] = acc[k];
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+    };
+    auto apply_cb = [&](const float *xb, u32x2 e) { cb_finish(cb_read(xb, e)); };
+    // SM_CB_PIPE: the decode of band q+1 (header readlanes, masks, addresses and its
+    // codebook reads -- the table is constant) runs inside band q, so the reads of band
+    // q+1 go out right after the barrier.
+    struct CbDec {
+        uint32_t xa[2], rl[2];
+        uint64_t live[2], cont[2];
+        float tv[2];
+    };
+    auto cb_decode = [&](u32x2 e) -> CbDec {
+        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
+        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
+        CbDec d;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
+            const uint32_t base = (h & kColMask) | (((h >> kCbOffShift) & kCbOffMask) << kCbColBits);
+            const uint32_t id = (wd[k] >> kCbColBits) & kCbDummyId;
+            d.live[k] = __ballot(id != kCbDummyId);
+            d.cont[k] = __ballot((int32_t)wd[k] < 0);
+            d.rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
+            d.xa[k] = wd[k] & kColMask;
+            d.tv[k] = tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+        }
+        return d;
+    };
+    auto cb_issue = [&](const float *xb, const CbDec &d) -> CbState {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        CbState st;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            st.xv[k] = xb[d.xa[k]];
+            st.yv[k] = yacc[d.rl[k]];
+            st.tv[k] = d.tv[k];
+            st.rl[k] = d.rl[k];
+            st.live[k] = d.live[k];
+            st.cont[k] = d.cont[k];
+        }
+        return st;
     };
 
     // Prologue, ordered so its memory latencies overlap: the first windows' x and entry
@@ -459,14 +521,31 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // dummies write nothing but the x buffers nobody reads any more (band2: and the
     // scratch slots).
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
+    [[maybe_unused]] CbDec dec;
+    if constexpr (kPipe) dec = cb_decode(E[0]);
     mark_phase(0);
     for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
             if (q + AX >= cw + 64) advance();
+            [[maybe_unused]] CbState st_rf;
             if constexpr (kDma) {
                 dma_x(q + 1, (u + 1) & 1);
+            } else if constexpr (kPipe) {
+                // sched_barrier: hipcc keeps the phases in this order (reads of band q,
+                // x stores, decode of band q+1), so the reads wait for nothing.
+                load_x(q + AX, X[u % AX]);
+                st_rf = cb_issue(xs[u & 1], dec);
+                __builtin_amdgcn_sched_barrier(0);
+                store_x((u + 1) & 1, X[(u + 1) % AX]);
+                __builtin_amdgcn_sched_barrier(0);
+                dec = cb_decode(E[(u + 1) % ER]);
+                __builtin_amdgcn_sched_barrier(0);
+            } else if constexpr (kRFirst) {
+                load_x(q + AX, X[u % AX]);
+                st_rf = cb_read(xs[u & 1], E[u % ER]);
+                store_x((u + 1) & 1, X[(u + 1) % AX]);
             } else {
                 load_x(q + AX, X[u % AX]);
                 store_x((u + 1) & 1, X[(u + 1) % AX]);
@@ -478,6 +557,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if constexpr (kEarly) E[(u + AE) % ER] = load_e(q + AE);
             if constexpr (ABL & 1) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
+            } else if constexpr (kRFirst || kPipe) {
+                cb_finish(st_rf);
             } else if constexpr (CB) {
                 apply_cb(xs[u & 1], E[u % ER]);
             } else {
