@@ -49,32 +49,38 @@ struct Seg {
 void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const int32_t *col,
                 const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom) {
     bool used[64] = {false};
-    const int wave = c >> 1, k = c & 1;
+    const int cpw = ids != nullptr ? geom.cpw : 2;
+    const int wave = c / cpw, k = c % cpw;
     const bool cb = ids != nullptr;
+    const uint32_t cb_colmask = (1u << geom.cb_col) - 1u, cb_dummy = geom.cb_dummy_word();
+    const int cb_off_shift = geom.cb_off_shift();
+    const bool tab_banks = cb && geom.tab_copies == 1;   // one table copy: bank = id mod 32
     const int32_t base = segs.empty() ? 0 : segs.front().rl;   // segments come in row order
     int next = 0;
-    // Bank use per half: x reads (column bank) and accumulator reads (row bank).
-    uint8_t xb[2][32] = {}, yb[2][32] = {};
+    // Bank use per half: x reads (column bank), accumulator reads (row bank) and, with
+    // one table copy, the table reads (id bank).
+    uint8_t xb[2][32] = {}, yb[2][32] = {}, tb[2][32] = {};
     // A segment's lanes read one accumulator (a broadcast): its row counts once per half.
-    auto note = [&](int lane, uint32_t cbits, int32_t rl, bool same_row_before) {
+    auto note = [&](int lane, uint32_t cbits, int32_t rl, bool same_row_before, uint32_t id) {
         const int h = lane >> 5;
         xb[h][cbits & 31]++;
         if (!(same_row_before && ((lane - 1) >> 5) == h)) yb[h][rl & 31]++;
+        tb[h][id & 31]++;
     };
     if (cb) {
-        const uint32_t h = ((uint32_t)base & ((1u << kCbColBits) - 1u)) | (kCbDummyId << kCbColBits) |
-                           ((((uint32_t)base >> kCbColBits) & kCbOffMask) << kCbOffShift);
-        band_ent[(size_t)(wave * 64) * 2 + k] = h ^ kCbDummyWord;
+        const uint32_t h = ((uint32_t)base & cb_colmask) | cb_dummy |
+                           ((((uint32_t)base >> geom.cb_col) & geom.cb_off_mask()) << cb_off_shift);
+        band_ent[(size_t)(wave * 64) * cpw + k] = h ^ cb_dummy;
         used[0] = true;
         next = 1;
-        note(0, h & ((1u << kCbColBits) - 1u), base + (int32_t)((h >> kCbOffShift) & kCbOffMask), false);
+        note(0, h & cb_colmask, base + (int32_t)((h >> cb_off_shift) & geom.cb_off_mask()), false, kCbDummyId);
     }
     auto put = [&](const Seg &g, int32_t j, int lane) {
         const uint32_t cbits = (uint32_t)(col[g.s + j] - clo_al);
         if (cb) {
-            const uint32_t w = cbits | ((uint32_t)ids[g.s + j] << kCbColBits) |
-                               ((uint32_t)(g.rl - base) << kCbOffShift) | ((j > 0 ? 1u : 0u) << kCbContBit);
-            band_ent[(size_t)(wave * 64 + lane) * 2 + k] = w ^ kCbDummyWord;
+            const uint32_t w = cbits | ((uint32_t)ids[g.s + j] << geom.cb_col) |
+                               ((uint32_t)(g.rl - base) << cb_off_shift) | ((j > 0 ? 1u : 0u) << kCbContBit);
+            band_ent[(size_t)(wave * 64 + lane) * cpw + k] = w ^ cb_dummy;
         } else {
             uint32_t *e = band_ent + ((size_t)(wave * 64 + lane)) * 4;
             e[k] = (cbits | ((uint32_t)j << geom.col_bits) | ((uint32_t)g.rl << (geom.col_bits + kB2RankBits))) ^
@@ -85,7 +91,7 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
             e[2 + k] = vb;
         }
         used[lane] = true;
-        note(lane, cbits, g.rl, j > 0);
+        note(lane, cbits, g.rl, j > 0, cb ? ids[g.s + j] : 0u);
     };
     for (const Seg &g : segs)
         if (g.n > 1)
@@ -97,18 +103,22 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
         if (g.n == 1) single.push_back(&g);
     const int ns = (int)single.size();
     if (ns == 0) return;
-    uint8_t xcnt[32] = {}, ycnt[32] = {};
-    std::vector<uint8_t> sx((size_t)ns), sy((size_t)ns), half((size_t)ns);
+    uint8_t xcnt[32] = {}, ycnt[32] = {}, tcnt[32] = {};
+    std::vector<uint8_t> sx((size_t)ns), sy((size_t)ns), st((size_t)ns), half((size_t)ns);
     for (int i = 0; i < ns; i++) {
         sx[(size_t)i] = (uint8_t)((col[single[(size_t)i]->s] - clo_al) & 31);
         sy[(size_t)i] = (uint8_t)(single[(size_t)i]->rl & 31);
+        st[(size_t)i] = tab_banks ? (uint8_t)(ids[single[(size_t)i]->s] & 31) : 0;
         xcnt[sx[(size_t)i]]++;
         ycnt[sy[(size_t)i]]++;
+        tcnt[st[(size_t)i]]++;
     }
     std::vector<int> order((size_t)ns);
     for (int i = 0; i < ns; i++) order[(size_t)i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-        return xcnt[sx[(size_t)a]] + ycnt[sy[(size_t)a]] > xcnt[sx[(size_t)b]] + ycnt[sy[(size_t)b]];
+        const int wa = xcnt[sx[(size_t)a]] + ycnt[sy[(size_t)a]] + (tab_banks ? tcnt[st[(size_t)a]] : 0);
+        const int wb = xcnt[sx[(size_t)b]] + ycnt[sy[(size_t)b]] + (tab_banks ? tcnt[st[(size_t)b]] : 0);
+        return wa > wb;
     });
     int free_in[2] = {0, 0};
     for (int l = 0; l < 64; l++)
@@ -118,13 +128,15 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
         for (int h = 0; h < 2; h++) {
             if (free_in[h] == 0) continue;
             const int a = xb[h][sx[(size_t)i]] + 1, b = yb[h][sy[(size_t)i]] + 1;
-            const int cost = 64 * (a * a + b * b) - free_in[h];
+            const int t = tab_banks ? tb[h][st[(size_t)i]] + 1 : 0;
+            const int cost = 64 * (a * a + b * b + t * t) - free_in[h];
             if (cost < bcost) { bcost = cost; best = h; }
         }
         half[(size_t)i] = (uint8_t)best;
         free_in[best]--;
         xb[best][sx[(size_t)i]]++;
         yb[best][sy[(size_t)i]]++;
+        tb[best][st[(size_t)i]]++;
     }
     int lane_next[2] = {31, 63};
     for (int i = 0; i < ns; i++) {
@@ -142,8 +154,9 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
     // Chunk capacity, longest segment and row span of one chunk.
     const int cap = cb ? kCbChunkTerms : 64;
     const int32_t max_seg = cb ? kCbChunkTerms : (int32_t)kB2DummyRank - 1;
-    const int32_t span = cb ? kCbRowSpan : INT32_MAX;
-    const size_t band_words = cb ? 2048 : 4096;
+    const int32_t span = cb ? geom.cb_row_span() : INT32_MAX;
+    const int nchunks = cb ? geom.chunks() : kB2Chunks;
+    const size_t band_words = cb ? (size_t)64 * nchunks : 4096;
     // A new chunk opens when the segment does not fit the current one (terms or rows).
     auto opens = [&](int fill, int32_t base, const Seg &g) {
         return fill + g.n > cap || g.rl - base >= span;
@@ -166,12 +179,16 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
     while (clo < c1 && count(clo, c1) > 0) {
         while (hist[(size_t)(clo - c0)] == 0) clo++;   // no band starts on an empty column
         const int64_t clo_al = clo & ~(int64_t)3;
+#ifdef SM_DEV_B2_WINDOW   // development A/B: narrower bands (fewer terms per band)
+        const int64_t lim = std::min<int64_t>(c1, clo_al + std::min<int32_t>(geom.window, SM_DEV_B2_WINDOW));
+#else
         const int64_t lim = std::min<int64_t>(c1, clo_al + geom.window);
+#endif
         // Largest chi <= lim with at most 32 * 64 terms (binary search on H).
         int64_t lo = clo + 1, hi = lim;
         while (lo < hi) {
             const int64_t mid = (lo + hi + 1) / 2;
-            if (count(clo, mid) <= (int64_t)kB2Chunks * 64) lo = mid; else hi = mid - 1;
+            if (count(clo, mid) <= (int64_t)nchunks * 64) lo = mid; else hi = mid - 1;
         }
         int64_t chi = lo;
         // A single column whose terms in this block need more than kB2Chunks chunks (a
@@ -200,14 +217,14 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
                 }
                 const Seg g{(int32_t)r, s, n};
                 if (opens(fill, base, g)) {
-                    if (single && chunks == kB2Chunks) { split = true; break; }   // rest: next band
+                    if (single && chunks == nchunks) { split = true; break; }   // rest: next band
                     chunks++; fill = 0; base = g.rl;
                 }
                 fill += n;
                 segs.push_back(g);
             }
             if (retry) continue;
-            if (chunks > kB2Chunks) {
+            if (chunks > nchunks) {
                 chi = clo + std::max<int64_t>(1, (chi - clo) * 31 / 32);
                 continue;
             }
@@ -217,7 +234,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
         const size_t base = out.ent.size();
         out.ent.resize(base + band_words, 0u);   // dummies: word 0 (= dummy ^ dummy), value 0
         out.clo.push_back((int32_t)clo_al);
-        chunk_segs.assign(kB2Chunks, {});
+        chunk_segs.assign((size_t)nchunks, {});
         int c = -1, fill = cap;
         int32_t cbase = 0;
         for (const Seg &g : segs) {
@@ -242,11 +259,12 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out = Band2Host();
     out.codebook = ids != nullptr;
     out.geom = geom;
-    if (geom.window > (1 << geom.col_bits) || (ids && geom.window > (1 << kCbColBits)) ||
+    if ((!ids && geom.cpw != 2) || geom.cpw < 1 || geom.cpw > 4 ||
+        geom.window > (1 << geom.col_bits) || (ids && geom.window > (1 << geom.cb_col)) ||
         geom.block_rows > ((int64_t)1 << (32 - geom.col_bits - kB2RankBits)) ||
-        geom.block_rows > ((int64_t)1 << (kCbColBits + kCbOffBits)))
+        geom.block_rows > ((int64_t)1 << (31 - kCbIdBits)))
         return false;
-    const int64_t band_words = ids ? 2048 : 4096;
+    const int64_t band_words = ids ? (int64_t)64 * geom.chunks() : 4096;
     if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)

@@ -316,9 +316,14 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 // Builds into `d` the balanced bands of an n_rows x n_cols CSR (the matrix's own, or
 // the hot column prefix of a relabeled graph); `forced`: keep mostly-padding bands.
+// Geometry (sm_build_opts.band_tall): 0 = wide (the default), 1 = tall; development
+// builds also take 3 = wide3 for codebook values (three chunks per wave, 12160-column
+// windows, one table copy; config 2: 38.5 vs 37.2 us wide -- the table's bank conflicts
+// cost what the third fewer bands save: 36.1 vs 36.2 us with the lookup ablated).
 static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
-                             bool tall, int32_t slabs, bool forced) {
+                             int32_t geo_opt, int32_t slabs, bool forced) {
+    const bool tall = geo_opt == 1;
     const B2Geom geom = !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
@@ -329,17 +334,28 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     std::vector<uint8_t> ids;
     const bool cb = kind == kXbCband && codebook_ids(val, nnz, table, ids);
     Band2Host bh;
-    const B2Geom g = !tall ? kB2Wide : cb ? kB2TallCb : kB2TallB2;
-    if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, g))
-        return SM_OK;
+#ifdef SM_DEV
+    const bool wide3 = cb && geo_opt == 3;
+#else
+    const bool wide3 = false;
+#endif
+    B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
+    // Bands are fixed slots of g.chunks() * 64 entries: where a slab's density leaves
+    // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
+    // bytes than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
+    auto fits = [&](const B2Geom &gg) {
+        if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, gg)) return false;
+        return forced || bh.n_bands == 0 ||
+               (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
+    };
+    bool ok = fits(g);
+    if (!ok && g.cpw == 3) {   // wide3 did not fit: the two-chunk wide geometry
+        g = kB2Wide;
+        ok = fits(g);
+    }
+    if (!ok) return SM_OK;
     std::vector<uint8_t>().swap(ids);
-    // Bands are fixed 2048-entry slots: where a slab's density leaves them mostly
-    // dummies (wide or very sparse matrices), the padding would cost more HBM bytes
-    // than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
-    if (!forced && bh.n_bands > 0 &&
-        (double)bh.real_terms < 0.7 * (double)bh.n_bands * kB2Chunks * 64)
-        return SM_OK;
-    const int64_t band_words = cb ? 2048 : 4096;
+    const int64_t band_words = cb ? (int64_t)64 * g.chunks() : 4096;
     const int64_t ntile = (int64_t)bh.n_blocks * bh.n_slabs;
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, bh.n_bands), m->device_bytes));
@@ -372,7 +388,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_bands = (int32_t)std::min<int64_t>(bh.n_bands, INT32_MAX);
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
-    d.n_chunks = bh.n_bands * kB2Chunks;
+    d.n_chunks = bh.n_bands * (cb ? g.chunks() : kB2Chunks);
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
     return SM_OK;
@@ -380,9 +396,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
 
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
-    // Geometry: band_tall = 1 takes the tall tiles (xband.h B2Geom).
+    // Geometry: band_tall (xband.h B2Geom, build_band2).
     return build_band2(m, m->plan.xb, m->n_rows, m->n_cols, m->nnz, rp, col, val, kind,
-                       m->opts.band_tall == 1, m->opts.band_slabs, kind_forced(m));
+                       m->opts.band_tall, m->opts.band_slabs, kind_forced(m));
 }
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
@@ -822,7 +838,7 @@ sm_status upload_sell_layouts(sm_matrix *m, const int32_t *rp, const int32_t *co
     }
     std::vector<int32_t>().swap(rcol);
     sm_status st = build_band2(m, p.hot, nr, H0, hot, rph.data(), ch.data(), vh.data(), kXbCband,
-                               false, 0, true);
+                               0, 0, true);
     if (st != SM_OK) return st;
     if (p.hot.n_blocks == 0 || p.hot.kind != kXbCband) {   // not applicable: sell serves all terms
         free_xband_dev(p.hot);

@@ -81,10 +81,7 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #define SM_E_EARLY 0
 #endif
 #ifndef SM_CB_RFIRST
-#define SM_CB_RFIRST 0
-#endif
-#ifndef SM_CB_PIPE
-#define SM_CB_PIPE 0
+#define SM_CB_RFIRST 1
 #endif
 #ifndef SM_X_AUX
 #define SM_X_AUX 0
@@ -93,6 +90,7 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #define SM_ENT_AUX kAuxNt
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 
 // ABL (development only, SM_BAND2_ABLATE; results wrong): 1 skips the apply,
 // 2 the x loads and stores, 4 the entry loads, 8 the slab hand-off (plain stores),
@@ -101,16 +99,20 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // per-band barrier (racy).
 // CB: the cband encoding (xband.h): one 32-bit word per term, values from the
 // codebook `table` (<= 255 entries), scaled by alpha once into LDS.
-// TALL: the tall geometry (xband.h B2Geom): 32K-row blocks, 4096 (cband 3840)
-// column windows, one float4 of x per lane per band.
-template <int ABL, int PRIO, bool CB, bool TALL>
+// GEO: the tile geometry (xband.h B2Geom): 0 wide; 1 tall (32K-row blocks, 4096 --
+// cband 3840 -- column windows, one float4 of x per lane per band); 2 wide3 (cband:
+// 12160-column windows, three chunks per wave per band, the table in one copy).
+template <int ABL, int PRIO, bool CB, int GEO>
 __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
-    constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : kB2Wide;
+    constexpr bool TALL = GEO == 1;
+    static_assert(GEO != 2 || CB, "wide3 is a cband geometry");
+    constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb : kB2Wide;
+    constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
     constexpr int W = G.window;
     constexpr int XV = (W + 4 * kB2Threads - 1) / (4 * kB2Threads);   // float4 of x per lane
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     constexpr uint32_t kRankMask = (1u << kB2RankBits) - 1u;
     // Every LDS byte counts in the tall geometry: band2 keeps per-lane scratch slots
     // for its dummy lanes' writes only in the wide one.
-    constexpr bool kScratch = !CB && !TALL;
+    constexpr bool kScratch = !CB && GEO == 0;
     // Rings: x window p+AX and the entries of band p+AE are loaded at band p into the
     // slots band p just freed (the x of window p was stored a band ago; the entries
     // of band p are loaded after its apply has decoded them).  Waiting for window p+1
@@ -131,17 +133,17 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // does not count the (asm) DMA, so its own wait for the entries of band q counts
     // only the AE-1 younger entry loads -- at least the 3 ops really pending then
     // (one entry load, the window's two DMA pieces) once AE >= 4: no extra stall.
-    constexpr bool kDma = CB && !TALL && SM_CB_DMA != 0;
+    constexpr bool kDma = CB && GEO == 0 && SM_CB_DMA != 0;
     static_assert(!kDma || SM_CB_DMA_EAHEAD >= 4, "DMA variant: hipcc's entry waits must not stall");
     constexpr int AX = kDma ? 1 : CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
     constexpr int AE = kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
     // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
     // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
     constexpr bool kEarly = SM_E_EARLY != 0;
-    // SM_CB_RFIRST (development A/B, wide cband): the apply's LDS reads go out before
-    // the next x window's LDS stores.
-    constexpr bool kRFirst = CB && !TALL && !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
-    constexpr bool kPipe = CB && !TALL && !kDma && !kEarly && SM_CB_PIPE != 0 && (ABL & ~3072) == 0;
+    // cband: the apply's LDS reads go out before the next x window's LDS stores, so
+    // they do not queue behind 16 waves' stores (config 2: 37.1 vs 39.6 us with the
+    // stores first; SM_CB_RFIRST=0 restores that order in development builds).
+    constexpr bool kRFirst = CB && !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
     constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
     constexpr int U0 = AX > ER ? AX : ER;
     constexpr int U = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
@@ -152,13 +154,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // kinds write only live lanes and use the LDS nearly to the last byte: their
     // hand-off words live in the x buffers once the band loop is over.
     __shared__ __attribute__((aligned(16))) float yacc[BROWS + (kScratch ? 64 : 0)];
-    __shared__ int32_t s_word_b2[kScratch ? 4 : 1];
     // cband: fl(table[id] * alpha) (0 past the table) in kTabCopies copies, entry id
     // of copy c at kTabCopies * id + c: lane l reads copy l % kTabCopies, so the
     // reads of a 32-lane group spread over the banks whatever the ids (wide: 32
     // copies, every group conflict-free -- 37.3 vs 38.1 us with 16, 39.1 with 8,
     // 38.6 with 4 on config 2; tall: one, no room for more).
-    constexpr int kTabCopies = TALL ? 1 : SM_CB_TAB_COPIES;
+    constexpr int kTabCopies = GEO == 0 ? SM_CB_TAB_COPIES : G.tab_copies;
     __shared__ float tab[CB ? 256 * kTabCopies : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t r0 = b * block_rows;
     const int32_t nr = min(block_rows, n_rows - r0);
     const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
-    constexpr uint32_t kBandBytes = CB ? 8192u : 16384u;   // entries of one band
+    constexpr uint32_t kBandBytes = CB ? 4096u * CPW : 16384u;   // entries of one band
     const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * (kBandBytes / 4), (uint64_t)nb * kBandBytes);
     // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi), read
     // by readlane; the window advances by 64 bands when the x loads reach its hi half.
@@ -260,11 +261,13 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     };
     // Entries of band q: band2 {word 2w, word 2w+1, value 2w, value 2w+1}, cband
     // {word 2w, word 2w+1} for this lane; past the tile: zeros = dummies.
-    using EV = typename std::conditional<CB, u32x2, u32x4>::type;
+    using EV = typename std::conditional<CB, typename std::conditional<CPW == 3, u32x3, u32x2>::type, u32x4>::type;
     auto load_e = [&](int32_t q) -> EV {
         const uint32_t off = kBandBytes * (uint32_t)q + (kBandBytes / kB2Threads) * (uint32_t)tid;
         if (ABL & 4) return EV{};
-        if constexpr (CB)
+        if constexpr (CB && CPW == 3)
+            return __builtin_amdgcn_raw_buffer_load_b96(e_src, off, 0, SM_ENT_AUX);
+        else if constexpr (CB)
             return __builtin_amdgcn_raw_buffer_load_b64(e_src, off, 0, SM_ENT_AUX);
         else
             return __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, SM_ENT_AUX);
@@ -335,28 +338,31 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // cband: row = chunk base (lane 0's header) + offset.  A segment's running sum
     // moves up one lane per round in lane (= column) order; the lanes a round updates
     // are an SGPR mask: the continuations whose predecessor finished last round.
-    // cband apply in two steps: cb_read decodes the chunk words and issues the six LDS
-    // reads, cb_finish adds and writes; the loop may put the next x window's LDS stores
-    // between them (SM_CB_RFIRST) so the reads do not queue behind 16 waves' stores.
+    // Two steps: cb_read decodes the chunk words and issues the 3 * CPW LDS reads,
+    // cb_finish adds and writes; the loop puts the next x window's LDS stores between
+    // them so the reads do not queue behind 16 waves' stores.
+    constexpr uint32_t kCbCol = (1u << G.cb_col) - 1u;
+    constexpr uint32_t kCbDummy = G.cb_dummy_word();
+    constexpr int kCbOffSh = G.cb_off_shift();
+    constexpr uint32_t kCbOffM = G.cb_off_mask();
     struct CbState {
-        float xv[2], yv[2], tv[2];
-        uint32_t rl[2];
-        uint64_t live[2], cont[2];
+        float xv[CPW], yv[CPW], tv[CPW];
+        uint32_t rl[CPW];
+        uint64_t live[CPW], cont[CPW];
     };
-    auto cb_read = [&](const float *xb, u32x2 e) -> CbState {
+    auto cb_read = [&](const float *xb, EV e) -> CbState {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
-        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
         CbState st;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
-            const uint32_t base = (h & kColMask) | (((h >> kCbOffShift) & kCbOffMask) << kCbColBits);
-            const uint32_t id = (wd[k] >> kCbColBits) & kCbDummyId;
+        for (int k = 0; k < CPW; ++k) {
+            const uint32_t wd = e[k] ^ kCbDummy;
+            const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd, 0);
+            const uint32_t base = (h & kCbCol) | (((h >> kCbOffSh) & kCbOffM) << G.cb_col);
+            const uint32_t id = (wd >> G.cb_col) & kCbDummyId;
             st.live[k] = __ballot(id != kCbDummyId);
-            st.cont[k] = __ballot((int32_t)wd[k] < 0);
-            st.rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
-            st.xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd[k] & kColMask)];
+            st.cont[k] = __ballot((int32_t)wd < 0);
+            st.rl[k] = base + ((wd >> kCbOffSh) & kCbOffM);
+            st.xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd & kCbCol)];
             st.tv[k] = (ABL & 32) ? __uint_as_float(id) : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
             st.yv[k] = yacc[st.rl[k]];
         }
@@ -364,72 +370,43 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     };
     auto cb_finish = [&](CbState st) {
         float *xv = st.xv, *yv = st.yv, *tv = st.tv;
-        uint32_t *rl = st.rl;
-        uint64_t *live = st.live, *cont = st.cont;
-        // Materialise all six reads before any write (one LDS wait per band).
-        asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
-        float tm[2], acc[2];
+        // Materialise all reads before any write (one LDS wait per band).
+        if constexpr (CPW == 3)
+            asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(xv[2]), "+v"(yv[0]), "+v"(yv[1]), "+v"(yv[2]),
+                         "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]));
+        else
+            asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
+        float tm[CPW], acc[CPW];
+        uint64_t R[CPW];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < CPW; ++k) {
             tm[k] = __fmul_rn(xv[k], tv[k]);
             acc[k] = __fadd_rn(yv[k], tm[k]);
+            R[k] = st.cont[k] & ~(st.cont[k] << 1);
         }
         if constexpr (!(ABL & 64)) {
-            uint64_t R0 = cont[0] & ~(cont[0] << 1), R1 = cont[1] & ~(cont[1] << 1);
-            while (R0 | R1) {
-                acc[0] = sel(R0, acc[0], __fadd_rn(shr1(acc[0]), tm[0]));
-                acc[1] = sel(R1, acc[1], __fadd_rn(shr1(acc[1]), tm[1]));
-                R0 = cont[0] & (R0 << 1);
-                R1 = cont[1] & (R1 << 1);
+            auto any = [&]() {
+                uint64_t a = 0;
+#pragma unroll
+                for (int k = 0; k < CPW; ++k) a |= R[k];
+                return a != 0;
+            };
+            while (any()) {
+#pragma unroll
+                for (int k = 0; k < CPW; ++k) {
+                    acc[k] = sel(R[k], acc[k], __fadd_rn(shr1(acc[k]), tm[k]));
+                    R[k] = st.cont[k] & (R[k] << 1);
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
-            const uint64_t last = live[k] & ~(cont[k] >> 1);
-            if ((last >> lane) & 1) yacc[rl[k]] = acc[k];
+        for (int k = 0; k < CPW; ++k) {   // the segment's last lane writes its row
+            const uint64_t last = st.live[k] & ~(st.cont[k] >> 1);
+            if ((last >> lane) & 1) yacc[st.rl[k]] = acc[k];
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
-    auto apply_cb = [&](const float *xb, u32x2 e) { cb_finish(cb_read(xb, e)); };
-    // SM_CB_PIPE: the decode of band q+1 (header readlanes, masks, addresses and its
-    // codebook reads -- the table is constant) runs inside band q, so the reads of band
-    // q+1 go out right after the barrier.
-    struct CbDec {
-        uint32_t xa[2], rl[2];
-        uint64_t live[2], cont[2];
-        float tv[2];
-    };
-    auto cb_decode = [&](u32x2 e) -> CbDec {
-        constexpr uint32_t kColMask = (1u << kCbColBits) - 1u;
-        const uint32_t wd[2] = {e.x ^ kCbDummyWord, e.y ^ kCbDummyWord};
-        CbDec d;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
-            const uint32_t base = (h & kColMask) | (((h >> kCbOffShift) & kCbOffMask) << kCbColBits);
-            const uint32_t id = (wd[k] >> kCbColBits) & kCbDummyId;
-            d.live[k] = __ballot(id != kCbDummyId);
-            d.cont[k] = __ballot((int32_t)wd[k] < 0);
-            d.rl[k] = base + ((wd[k] >> kCbOffShift) & kCbOffMask);
-            d.xa[k] = wd[k] & kColMask;
-            d.tv[k] = tab[id * kTabCopies + (lane & (kTabCopies - 1))];
-        }
-        return d;
-    };
-    auto cb_issue = [&](const float *xb, const CbDec &d) -> CbState {
-        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        CbState st;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            st.xv[k] = xb[d.xa[k]];
-            st.yv[k] = yacc[d.rl[k]];
-            st.tv[k] = d.tv[k];
-            st.rl[k] = d.rl[k];
-            st.live[k] = d.live[k];
-            st.cont[k] = d.cont[k];
-        }
-        return st;
-    };
+    auto apply_cb = [&](const float *xb, EV e) { cb_finish(cb_read(xb, e)); };
 
     // Prologue, ordered so its memory latencies overlap: the first windows' x and entry
     // loads go out first, then the codebook and (slab 0) y loads; the LDS writes of all
@@ -521,8 +498,6 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // dummies write nothing but the x buffers nobody reads any more (band2: and the
     // scratch slots).
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
-    [[maybe_unused]] CbDec dec;
-    if constexpr (kPipe) dec = cb_decode(E[0]);
     mark_phase(0);
     for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
@@ -532,16 +507,6 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             [[maybe_unused]] CbState st_rf;
             if constexpr (kDma) {
                 dma_x(q + 1, (u + 1) & 1);
-            } else if constexpr (kPipe) {
-                // sched_barrier: hipcc keeps the phases in this order (reads of band q,
-                // x stores, decode of band q+1), so the reads wait for nothing.
-                load_x(q + AX, X[u % AX]);
-                st_rf = cb_issue(xs[u & 1], dec);
-                __builtin_amdgcn_sched_barrier(0);
-                store_x((u + 1) & 1, X[(u + 1) % AX]);
-                __builtin_amdgcn_sched_barrier(0);
-                dec = cb_decode(E[(u + 1) % ER]);
-                __builtin_amdgcn_sched_barrier(0);
             } else if constexpr (kRFirst) {
                 load_x(q + AX, X[u % AX]);
                 st_rf = cb_read(xs[u & 1], E[u % ER]);
@@ -557,7 +522,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if constexpr (kEarly) E[(u + AE) % ER] = load_e(q + AE);
             if constexpr (ABL & 1) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
-            } else if constexpr (kRFirst || kPipe) {
+            } else if constexpr (kRFirst) {
                 cb_finish(st_rf);
             } else if constexpr (CB) {
                 apply_cb(xs[u & 1], E[u % ER]);
@@ -609,11 +574,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         flush_prof();
         return;
     }
-    int32_t *s_word = s_word_b2;
-    if constexpr (!kScratch) {   // every wave is past its last x read
-        __syncthreads();
-        s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
-    }
+    __syncthreads();   // every wave is past its last x read: the hand-off words live there
+    int32_t *s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
     slab_handoff<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
                              nr, slab, n_slabs, y_vec);
     flush_prof();
@@ -625,8 +587,9 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
                              float *y, float alpha, float beta, hipStream_t s) {
     if (xb.n_blocks <= 0) return hipSuccess;
     const bool cb = xb.kind == kXbCband;
-    const bool tall = xb.band_cols != kB2Wide.window;
-    const B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+    const bool wide3 = cb && xb.band_cols == kB2Wide3Cb.window;
+    const bool tall = !wide3 && xb.band_cols != kB2Wide.window;
+    const B2Geom g = wide3 ? kB2Wide3Cb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -654,40 +617,51 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         const char *e = dev_env("SM_BAND2_PRIO");
         return e ? atoi(e) : 2;
     }();
+    if (wide3) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true, 2); break;
+        case 4: SM_B2(4, 2, true, 2); break;
+        case 8: SM_B2(8, 2, true, 2); break;
+        case 32: SM_B2(32, 2, true, 2); break;
+        case 2048: SM_B2(2048, 2, true, 2); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (tall) {
         if (abl == 8) {
-            if (cb) SM_B2(8, 2, true, true); else SM_B2(8, 2, false, true);
+            if (cb) SM_B2(8, 2, true, 1); else SM_B2(8, 2, false, 1);
             return hipGetLastError();
         }
         if (abl != 0) return hipErrorInvalidValue;
-        if (cb) SM_B2(0, 2, true, true); else SM_B2(0, 2, false, true);
+        if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
         return hipGetLastError();
     }
     if (cb) {
         switch (abl) {
         case 0:
-            if (prio == 0) SM_B2(0, 0, true, false);
-            else if (prio == 1) SM_B2(0, 1, true, false);
-            else if (prio == 3) SM_B2(0, 3, true, false);
-            else SM_B2(0, 2, true, false);
+            if (prio == 0) SM_B2(0, 0, true, 0);
+            else if (prio == 1) SM_B2(0, 1, true, 0);
+            else if (prio == 3) SM_B2(0, 3, true, 0);
+            else SM_B2(0, 2, true, 0);
             break;
-        case 1: SM_B2(1, 2, true, false); break;
-        case 2: SM_B2(2, 2, true, false); break;
-        case 4: SM_B2(4, 2, true, false); break;
-        case 8: SM_B2(8, 2, true, false); break;
-        case 32: SM_B2(32, 2, true, false); break;
-        case 64: SM_B2(64, 2, true, false); break;
-        case 128: SM_B2(128, 2, true, false); break;
-        case 256: SM_B2(256, 2, true, false); break;
-        case 512: SM_B2(512, 2, true, false); break;
-        case 516: SM_B2(516, 2, true, false); break;
-        case 513: SM_B2(513, 2, true, false); break;
+        case 1: SM_B2(1, 2, true, 0); break;
+        case 2: SM_B2(2, 2, true, 0); break;
+        case 4: SM_B2(4, 2, true, 0); break;
+        case 8: SM_B2(8, 2, true, 0); break;
+        case 32: SM_B2(32, 2, true, 0); break;
+        case 64: SM_B2(64, 2, true, 0); break;
+        case 128: SM_B2(128, 2, true, 0); break;
+        case 256: SM_B2(256, 2, true, 0); break;
+        case 512: SM_B2(512, 2, true, 0); break;
+        case 516: SM_B2(516, 2, true, 0); break;
+        case 513: SM_B2(513, 2, true, 0); break;
         case 1024: {
             unsigned long long h[8] = {};
             void *sym = nullptr;
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_prof)) != hipSuccess) return hipErrorInvalidValue;
             (void)hipMemsetAsync(sym, 0, sizeof(h), s);
-            SM_B2(1024, 2, true, false);
+            SM_B2(1024, 2, true, 0);
             (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
             const double w = (double)h[7], bands = (double)h[6] / w;
@@ -701,7 +675,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             std::vector<unsigned long long> h((size_t)3 * nt);
             void *sym = nullptr;
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
-            SM_B2(2048, 2, true, false);
+            SM_B2(2048, 2, true, 0);
             (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
             unsigned long long t0 = ~0ull;
@@ -736,20 +710,21 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     }
     switch (abl) {
     case 0:
-        if (prio == 0) SM_B2(0, 0, false, false); else SM_B2(0, 2, false, false);
+        if (prio == 0) SM_B2(0, 0, false, 0); else SM_B2(0, 2, false, 0);
         break;
-    case 1: SM_B2(1, 2, false, false); break;
-    case 2: SM_B2(2, 2, false, false); break;
-    case 4: SM_B2(4, 2, false, false); break;
-    case 8: SM_B2(8, 2, false, false); break;
-    case 16: SM_B2(16, 2, false, false); break;
+    case 1: SM_B2(1, 2, false, 0); break;
+    case 2: SM_B2(2, 2, false, 0); break;
+    case 4: SM_B2(4, 2, false, 0); break;
+    case 8: SM_B2(8, 2, false, 0); break;
+    case 16: SM_B2(16, 2, false, 0); break;
     default: return hipErrorInvalidValue;
     }
 #else
+    if (wide3) return hipErrorInvalidValue;   // development builds only
     if (tall) {
-        if (cb) SM_B2(0, 2, true, true); else SM_B2(0, 2, false, true);
+        if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {
-        if (cb) SM_B2(0, 2, true, false); else SM_B2(0, 2, false, false);
+        if (cb) SM_B2(0, 2, true, 0); else SM_B2(0, 2, false, 0);
     }
 #endif
 #undef SM_B2

@@ -106,13 +106,28 @@ static_assert(kB2Window <= (1 << kCbColBits), "window column fits the column fie
 // and 4096-column windows (cband: 3840, its table takes 1 KiB) -- half the x per
 // term of a tile, twice the slabs for the same tile count.  band2 word: column
 // (col_bits) | rank (4) | row (32 - col_bits - 4).
+// wide3 (cband only): 16K-row blocks, 12160-column windows and three chunks per wave
+// per band (48 chunks, 3072 terms): a third fewer bands -- each band pays a fixed
+// barrier-and-latency chain -- in the same LDS (64 KiB of sums, two 47.5 KiB x
+// windows, the table in ONE copy: its bank conflicts are spread by the builder like
+// those of the x and accumulator reads).  Its cband word: column (14) | id (8) | row
+// - base (9: a chunk's rows span < 512) | continuation (1).
 struct B2Geom {
     int32_t block_rows, window, col_bits;
+    int32_t cpw = 2;          // chunks per wave per band
+    int32_t cb_col = kCbColBits;   // cband column bits (row offset: 23 - cb_col bits)
+    int32_t tab_copies = 32;  // cband: LDS copies of the scaled table (kernel)
     constexpr uint32_t dummy_word() const { return kB2DummyRank << col_bits; }
+    constexpr int chunks() const { return 16 * cpw; }
+    constexpr uint32_t cb_dummy_word() const { return kCbDummyId << cb_col; }
+    constexpr int cb_off_shift() const { return cb_col + kCbIdBits; }
+    constexpr uint32_t cb_off_mask() const { return (1u << (31 - kCbIdBits - cb_col)) - 1u; }
+    constexpr int32_t cb_row_span() const { return 1 << (31 - kCbIdBits - cb_col); }
 };
 constexpr B2Geom kB2Wide{1 << 14, 8192, 14};
 constexpr B2Geom kB2TallB2{1 << 15, 4096, 13};
-constexpr B2Geom kB2TallCb{1 << 15, 3840, 13};
+constexpr B2Geom kB2TallCb{1 << 15, 3840, 13, 2, kCbColBits, 1};
+constexpr B2Geom kB2Wide3Cb{1 << 14, 12160, 14, 3, 14, 1};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

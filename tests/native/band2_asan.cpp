@@ -103,7 +103,12 @@ static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int
     Band2Host h;
     if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data(), geom)) {
         printf("FAIL cband build\n"); return 1; }
-    if (!h.codebook || (int64_t)h.ent.size() != h.n_bands * 2048) { printf("FAIL cband sizes\n"); return 1; }
+    const int cpw = geom.cpw, nch = geom.chunks();
+    const size_t bw = (size_t)64 * nch;
+    const uint32_t dmy = geom.cb_dummy_word(), cmask = (1u << geom.cb_col) - 1u;
+    const int osh = geom.cb_off_shift();
+    const uint32_t omask = geom.cb_off_mask();
+    if (!h.codebook || h.ent.size() != (size_t)h.n_bands * bw) { printf("FAIL cband sizes\n"); return 1; }
     std::vector<std::vector<std::pair<int32_t, float>>> got(n_rows);
     int64_t terms = 0;
     for (int64_t t = 0; t < (int64_t)h.n_blocks * h.n_slabs; t++) {
@@ -111,28 +116,28 @@ static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int
         const int64_t c0 = s * h.slab_cols, c1 = std::min<int64_t>(n_cols, c0 + h.slab_cols);
         for (int64_t g = h.tile_band_start[t]; g < h.tile_band_start[t + 1]; g++) {
             const int64_t clo = h.band_clo[g];
-            for (int c = 0; c < kB2Chunks; c++) {
-                const int wave = c >> 1, k = c & 1;
-                auto word = [&](int l) { return h.ent[(size_t)g * 2048 + (size_t)(wave * 64 + l) * 2 + k] ^ kCbDummyWord; };
+            for (int c = 0; c < nch; c++) {
+                const int wave = c / cpw, k = c % cpw;
+                auto word = [&](int l) { return h.ent[(size_t)g * bw + (size_t)(wave * 64 + l) * cpw + k] ^ dmy; };
                 const uint32_t hd = word(0);
-                if (((hd >> kCbColBits) & kCbDummyId) != kCbDummyId) { printf("FAIL header id\n"); return 1; }
-                const uint32_t base = (hd & ((1u << kCbColBits) - 1u)) | (((hd >> kCbOffShift) & kCbOffMask) << kCbColBits);
+                if (((hd >> geom.cb_col) & kCbDummyId) != kCbDummyId) { printf("FAIL header id\n"); return 1; }
+                const uint32_t base = (hd & cmask) | (((hd >> osh) & omask) << geom.cb_col);
                 if (hd >> kCbContBit) { printf("FAIL header cont\n"); return 1; }
                 std::vector<int> rows_seen;
                 int prev_row = -1;
                 for (int l = 1; l < 64; l++) {
                     const uint32_t w = word(l);
-                    const uint32_t id = (w >> kCbColBits) & kCbDummyId;
+                    const uint32_t id = (w >> geom.cb_col) & kCbDummyId;
                     if (id == kCbDummyId) {
-                        if (w != kCbDummyWord) { printf("FAIL cband dummy\n"); return 1; }
+                        if (w != dmy) { printf("FAIL cband dummy\n"); return 1; }
                         prev_row = -1;
                         continue;
                     }
                     if (id >= table.size()) { printf("FAIL id range\n"); return 1; }
-                    const uint32_t rl = base + ((w >> kCbOffShift) & kCbOffMask);
+                    const uint32_t rl = base + ((w >> osh) & omask);
                     const bool cont = (w >> kCbContBit) != 0;
                     const int64_t r = b * h.block_rows + rl;
-                    const int64_t cc = clo + (w & ((1u << kCbColBits) - 1u));
+                    const int64_t cc = clo + (w & cmask);
                     if (r >= n_rows || (int64_t)rl >= h.block_rows) { printf("FAIL cband row\n"); return 1; }
                     if (cc - clo >= geom.window || cc < c0 || cc >= c1) { printf("FAIL cband window\n"); return 1; }
                     const int seen = (int)std::count(rows_seen.begin(), rows_seen.end(), (int)rl);
@@ -178,6 +183,7 @@ static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned se
         }
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2TallCb);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Wide3Cb);
     }
     return bad;
 }
@@ -205,6 +211,7 @@ int main() {
         bad += check_layout(rp, col, val, n_rows, n_cols, 1, true);
         bad += check_layout(rp, col, val, n_rows, n_cols, 5, true);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, 1);   // 40-term segments fit a chunk
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, 1, kB2Wide3Cb);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, 5);
     }
     // Rows of 70 consecutive columns: cband cuts bands inside them (<= 63 terms).
@@ -252,6 +259,7 @@ int main() {
         bad += check_layout(rp, col, val, n_rows, n_cols, slabs, true, kB2TallB2);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2TallCb);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Wide3Cb);
     }
     // More than 255 distinct values: no codebook.
     {
