@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // cband: the apply's LDS reads go out before the next x window's LDS stores, so
     // they do not queue behind 16 waves' stores (config 2: 37.1 vs 39.6 us with the
     // stores first; SM_CB_RFIRST=0 restores that order in development builds).
-    constexpr bool kRFirst = CB && !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
+    constexpr bool kRFirst = !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
     constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
     constexpr int U0 = AX > ER ? AX : ER;
     constexpr int U = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
@@ -280,32 +280,45 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         return (uint32_t)__builtin_amdgcn_update_dpp((int)kB2DummyRank, (int)v, 0x130, 0xF, 0xF, false);
     };
     (void)kB2Dummy;
-    auto apply_b2 = [&](const float *xb, u32x4 e) {
-        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        const uint32_t wd[2] = {e.x ^ kB2Dummy, e.y ^ kB2Dummy};
-        const float va[2] = {__uint_as_float(e.z), __uint_as_float(e.w)};
-        float xv[2], yv[2];
+    // band2 apply in two steps like cband's (b2_read issues the four LDS reads, the
+    // loop stores the next x window, b2_finish adds and writes).
+    struct B2State {
+        float xv[2], yv[2], va[2];
         uint32_t rk[2], rl[2];
         bool live[2];
-        bool more = false;
+        bool more;
+    };
+    auto b2_read = [&](const float *xb, u32x4 e) -> B2State {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        const uint32_t wd[2] = {e.x ^ kB2Dummy, e.y ^ kB2Dummy};
+        B2State st;
+        st.va[0] = __uint_as_float(e.z);
+        st.va[1] = __uint_as_float(e.w);
+        st.more = false;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            rk[k] = (wd[k] >> kB2Col) & kRankMask;
-            live[k] = rk[k] != kB2DummyRank;
-            rl[k] = wd[k] >> (kB2Col + kB2RankBits);   // dummies decode to row 0, column 0
-            xv[k] = xb[wd[k] & kColMask];
-            yv[k] = yacc[rl[k]];
-            more |= live[k] && rk[k] > 0;
+            st.rk[k] = (wd[k] >> kB2Col) & kRankMask;
+            st.live[k] = st.rk[k] != kB2DummyRank;
+            st.rl[k] = wd[k] >> (kB2Col + kB2RankBits);   // dummies decode to row 0, column 0
+            st.xv[k] = xb[wd[k] & kColMask];
+            st.yv[k] = yacc[st.rl[k]];
+            st.more |= st.live[k] && st.rk[k] > 0;
         }
+        return st;
+    };
+    auto b2_finish = [&](B2State st) {
+        float *xv = st.xv, *yv = st.yv;
+        const uint32_t *rk = st.rk, *rl = st.rl;
+        const bool *live = st.live;
         // Materialise all four reads before any write (one LDS wait per band).
         asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]));
         float tm[2], acc[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            tm[k] = __fmul_rn(xv[k], __fmul_rn(va[k], alpha));
+            tm[k] = __fmul_rn(xv[k], __fmul_rn(st.va[k], alpha));
             acc[k] = __fadd_rn(yv[k], tm[k]);
         }
-        if (__any(more)) {
+        if (__any(st.more)) {
             for (uint32_t r = 1;; ++r) {
                 bool again = false;
 #pragma unroll
@@ -327,6 +340,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
+    auto apply_b2 = [&](const float *xb, u32x4 e) { b2_finish(b2_read(xb, e)); };
 
     // Lane select by an SGPR lane mask (v_cndmask_b32 with the mask as its condition):
     // lane i takes b where bit i of m is set, else a.
@@ -504,12 +518,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
             if (q + AX >= cw + 64) advance();
-            [[maybe_unused]] CbState st_rf;
+            using RState = typename std::conditional<CB, CbState, B2State>::type;
+            [[maybe_unused]] RState st_rf;
             if constexpr (kDma) {
                 dma_x(q + 1, (u + 1) & 1);
             } else if constexpr (kRFirst) {
                 load_x(q + AX, X[u % AX]);
-                st_rf = cb_read(xs[u & 1], E[u % ER]);
+                if constexpr (CB) st_rf = cb_read(xs[u & 1], E[u % ER]);
+                else st_rf = b2_read(xs[u & 1], E[u % ER]);
                 store_x((u + 1) & 1, X[(u + 1) % AX]);
             } else {
                 load_x(q + AX, X[u % AX]);
@@ -523,7 +539,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             if constexpr (ABL & 1) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
             } else if constexpr (kRFirst) {
-                cb_finish(st_rf);
+                if constexpr (CB) cb_finish(st_rf);
+                else b2_finish(st_rf);
             } else if constexpr (CB) {
                 apply_cb(xs[u & 1], E[u % ER]);
             } else {
