@@ -11,8 +11,10 @@
 //
 // Per band p, every wave (static register rings, the loop unrolled by 2):
 //   load x window p+2 into registers (two float4 per lane),
-//   store x window p+1 (loaded a band ago) into the free LDS buffer,
-//   apply band p: term = x_lds[col] * (v * alpha), the chunk's terms added to the
+//   issue band p's LDS reads (x, codebook value, accumulator of each chunk),
+//   store x window p+1 (loaded a band ago) into the free LDS buffer -- after the
+//   reads, so they do not queue behind 16 waves' stores,
+//   finish band p: term = x_lds[col] * (v * alpha), the chunk's terms added to the
 //   LDS accumulators in rank rounds (a row's segment runs up consecutive lanes by
 //   DPP, its last lane writes; no two lanes touch one row in a round, no atomics),
 //   load the entries of band p+2 (into the registers band p's entries held),
