@@ -15,7 +15,7 @@ OBJS      = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) \
             $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS      = include/sparsematrix.h $(wildcard $(CSRC)/*.h)
 
-all: $(LIB) $(SHIM) oracle compat build/blas_test
+all: $(LIB) $(SHIM) oracle compat build/blas_test build/sblas_addmatmat
 
 # C++ drop-in shim (reference class/kernel signatures) over the C ABI
 $(SHIM): $(CSRC)/sblas_shim.cpp include/sblas/sparse-matrix.h include/sblas/kernel.h $(LIB)
@@ -40,7 +40,13 @@ endif
 # The reference harness's command line over the GPU backend (tools/blas_test.cc).
 build/blas_test: tools/blas_test.cc include/sblas/sparse-matrix.h $(SHIM)
 	@mkdir -p build
-	$(HIPCC) -O2 -std=c++17 -Iinclude/sblas -o $@ $< -L$(PKG) -lsblas -lsparsematrix_amd \
+	$(HIPCC) -O2 -std=c++17 -Iinclude/sblas -Iinclude -o $@ $< -L$(PKG) -lsblas -lsparsematrix_amd \
+	    -Wl,-rpath,'$$ORIGIN/../$(PKG)'
+
+# One AddMatMat through the C++ surface (tests/test_gpu_shim.py).
+build/sblas_addmatmat: tools/sblas_addmatmat.cc include/sblas/sparse-matrix.h include/sparsematrix.h $(SHIM)
+	@mkdir -p build
+	$(HIPCC) -O2 -std=c++17 -Iinclude/sblas -Iinclude -o $@ $< -L$(PKG) -lsblas -lsparsematrix_amd \
 	    -Wl,-rpath,'$$ORIGIN/../$(PKG)'
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)

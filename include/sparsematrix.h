@@ -79,10 +79,17 @@ typedef enum sm_algo {
     SM_ALGO_SELL = 5,     /* sorted sliced-ELL, one lane per row (every row up to 2048
                              terms bit-identical; longer rows in 2048-term segments whose
                              sums are added in order); STREAM when not built           */
-    SM_ALGO_NATIVE = 6    /* the reference's own stream (uint8 deltas + ids, 256-column
+    SM_ALGO_NATIVE = 6,   /* the reference's own stream (uint8 deltas + ids, 256-column
                              panels) decoded on the device; bit-identical for every
                              output; only for matrices built from the dense index
                              (SM_ERR_NOT_SUPPORTED otherwise)                          */
+    SM_ALGO_EXACT = 7     /* the fastest kernel built for the matrix that adds every
+                             output's terms in the reference's order (bit-identical):
+                             the column-swept or one-slab band layout, the column-chunked
+                             or segment-free sliced ELL, the stream kernel when no row
+                             exceeds SM_SERIAL_ROW_MAX terms, else PARITY.  SpMM and
+                             AddMatMat with m > 1: the row-panel kernels (every row in
+                             order).  What the reference's C++ surface (libsblas) runs. */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the
@@ -124,6 +131,10 @@ typedef struct sm_info {
                                    before the sliced ELL adds the other terms (AUTO, SELL)  */
     int32_t sweep_blocks;       /* row blocks of the column-swept layout (0: not built); it
                                    serves SpMV when built (AUTO): every row bit-identical    */
+    int64_t exact_sell_slices;  /* slices of the unsegmented sliced ELL (sm_build_opts.exact_sell;
+                                   0: not built) that SM_ALGO_EXACT runs                   */
+    int32_t exact_algo;         /* the sm_algo SM_ALGO_EXACT runs for a 16-byte aligned x
+                                   (SM_ALGO_SELL also for the unsegmented sliced ELL)       */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -212,7 +223,10 @@ typedef struct sm_build_opts {
                                   hottest this many relabeled columns through codebook bands
                                   with x in LDS, the rest through the sliced ELL (within the
                                   Sum|terms| bound); 0 / -1 never (slower on R-MAT 24)     */
-    int32_t reserved_opts;
+    int32_t exact_sell;        /* an unsegmented sorted sliced ELL beside the layout above, for
+                                  SM_ALGO_EXACT when no built layout keeps the reference's order
+                                  for every row: 0 auto (matrices from the dense index, i.e.
+                                  the reference's CopyForm path), 1 always, -1 never        */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);
@@ -284,13 +298,14 @@ SM_API sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const f
  * SpMM in the matrix's workspace, asynchronous on `stream`: the stream first waits on
  * an event recorded after the previous call's last use of the workspace (calls from
  * any streams take turns on the device; the host blocks only when a larger m makes
- * the workspace grow).  Otherwise one thread per output reads A and C in place. */
+ * the workspace grow); m > 128: the same per group of 128 rows of A and C.
+ * SM_ALGO_PARITY: one thread per output reads A and C in place. */
 SM_API sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
                               float *c, int32_t ldc, float alpha, float beta, sm_algo algo,
                               sm_stream stream);
 
-/* Synchronous drop-in for AddMatMat on HOST pointers (uploads A and C,
- * computes with SM_ALGO_PARITY, downloads C).  Bit-identical to the reference. */
+/* Synchronous drop-in for AddMatMat on HOST pointers (uploads A and C, computes with
+ * SM_ALGO_EXACT, downloads C).  Bit-identical to the reference. */
 SM_API sm_status sm_addmatmat_host(const sm_matrix *mat, const float *a, int32_t m, int32_t lda,
                                    float *c, int32_t ldc, float alpha, float beta);
 
@@ -324,8 +339,10 @@ SM_API sm_status sm_stream_sync(sm_stream stream);
  * slices (SpMM: of the X panel's row slices) over xGMI into the context's buffer,
  * then the local SpMV / SpMM on the same stream.  No other collective: the reference's
  * panels already write disjoint outputs (sparse-matrix.cc:164-190).
- * RCCL is loaded at run time (the copy already in the process if any); without it
- * sm_multi_* return SM_ERR_NOT_SUPPORTED.  Errors: sm_multi_last_error(). */
+ * RCCL is loaded at run time (the copy already in the process if any, else
+ * $SM_RCCL_LIB if set, else the system's); without it sm_multi_create returns
+ * SM_ERR_NOT_SUPPORTED (sm_multi_create_with takes any all-gather instead).
+ * Errors: sm_multi_last_error(). */
 #define SM_UNIQUE_ID_BYTES 128
 typedef struct sm_unique_id { char internal[SM_UNIQUE_ID_BYTES]; } sm_unique_id;
 typedef struct sm_multi sm_multi;
@@ -342,6 +359,22 @@ SM_API sm_status sm_multi_unique_id(sm_unique_id *id);
  * `local` (not owned; keep it alive) and joins the communicator on its device. */
 SM_API sm_status sm_multi_create(const sm_unique_id *id, int32_t nranks, int32_t rank,
                                  const sm_matrix *local, sm_multi **out);
+/* A caller-supplied all-gather instead of RCCL (no reference equivalent: the reference
+ * has no multi-device path).  `allgather` gathers `count` floats from every rank's
+ * `send` into `recv` in rank order (rank r's slice at recv + r*count), ordered on
+ * `stream` (a hipStream_t): it may enqueue device work on `stream`, or synchronise
+ * `stream` and block the host until `recv` holds the result (a host-staged gather over
+ * MPI, gloo, ...).  It returns 0 on success.  Everything else -- the partition, the two
+ * gather buffers, their stream ordering, the pipelined batch -- is the context's, as
+ * with RCCL.  sm_multi_unique_id is not needed. */
+typedef int32_t (*sm_allgather_fn)(const float *send, float *recv, int64_t count,
+                                   sm_stream stream, void *user);
+typedef struct sm_collective {
+    sm_allgather_fn allgather;
+    void *user;   /* passed back to every call */
+} sm_collective;
+SM_API sm_status sm_multi_create_with(const sm_collective *coll, int32_t nranks, int32_t rank,
+                                      const sm_matrix *local, sm_multi **out);
 SM_API void sm_multi_destroy(sm_multi *mc);
 /* y_local = alpha * B_local * x + beta * y_local, x = all-gather of the x_local slices. */
 SM_API sm_status sm_multi_spmv(sm_multi *mc, float alpha, const float *x_local, float beta,
@@ -361,7 +394,13 @@ SM_API sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, const sm_matri
                                      float alpha, const float *const *x_local, float beta,
                                      float *const *y_local, sm_algo algo, sm_stream stream);
 /* The all-gather alone (n_rhs = 1 for x), into the context's buffer; *x_full (optional)
- * receives its device address, valid until the next call on the context. */
+ * receives its device address, valid until the next call on the context (which waits
+ * for the work queued on `stream` up to this call, not for reads the caller adds later
+ * on other streams).
+ * Buffer ordering: every product records, on the stream that ran it, that it has read
+ * the gathered x; any later all-gather into that buffer waits for it, from whatever
+ * stream.  Calls on one context therefore may come from several streams.  Inside a
+ * stream capture, the captured products are ordered by the capture only. */
 SM_API sm_status sm_multi_allgather(sm_multi *mc, const float *x_local, int32_t n_rhs,
                                     sm_stream stream, const float **x_full);
 /* Device timing of sm_multi_spmv / _spmm (HIP events around the all-gather and the

@@ -31,7 +31,8 @@ SM_ERR_NO_DEVICE = 7
 
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
-ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5, "native": 6}
+ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5, "native": 6,
+         "exact": 7}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
@@ -45,7 +46,7 @@ EXPORTS = (
     "sm_addmatmat_host", "sm_beta_scale", "sm_transpose", "sm_panel_kernel", "sm_stream_sync",
     "sm_multi_last_error", "sm_multi_partition", "sm_multi_unique_id", "sm_multi_create",
     "sm_multi_destroy", "sm_multi_spmv", "sm_multi_spmm", "sm_multi_spmv_batch",
-    "sm_multi_allgather", "sm_multi_set_timing", "sm_multi_last_times",
+    "sm_multi_allgather", "sm_multi_set_timing", "sm_multi_last_times", "sm_multi_create_with",
 )
 
 SM_UNIQUE_ID_BYTES = 128
@@ -53,6 +54,14 @@ SM_UNIQUE_ID_BYTES = 128
 
 class SmUniqueId(C.Structure):
     _fields_ = [("internal", C.c_char * SM_UNIQUE_ID_BYTES)]
+
+
+# sm_allgather_fn / sm_collective (include/sparsematrix.h): a caller-supplied all-gather.
+SmAllgatherFn = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
+
+
+class SmCollective(C.Structure):
+    _fields_ = [("allgather", SmAllgatherFn), ("user", C.c_void_p)]
 
 
 class SmInfo(C.Structure):
@@ -66,6 +75,7 @@ class SmInfo(C.Structure):
         ("device_bytes", C.c_int64), ("col_relabel", C.c_int32), ("xband_slab_cols", C.c_int32),
         ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("ccsell_chunks", C.c_int32),
         ("hot_cols", C.c_int32), ("sweep_blocks", C.c_int32),
+        ("exact_sell_slices", C.c_int64), ("exact_algo", C.c_int32),
     ]
 
 
@@ -81,7 +91,7 @@ class SmBuildOpts(C.Structure):
         ("sell_codebook", C.c_int32), ("sell_max_len", C.c_int32), ("sell_streams", C.c_int32),
         ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
         ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32), ("hot_cols", C.c_int32),
-        ("reserved_opts", C.c_int32),
+        ("exact_sell", C.c_int32),
     ]
 
 
@@ -151,6 +161,7 @@ def _declare(L):
         "sm_multi_partition": ([_i64, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
         "sm_multi_unique_id": ([C.POINTER(SmUniqueId)], C.c_int),
         "sm_multi_create": ([C.POINTER(SmUniqueId), _i32, _i32, _vp, C.POINTER(_vp)], C.c_int),
+        "sm_multi_create_with": ([C.POINTER(SmCollective), _i32, _i32, _vp, C.POINTER(_vp)], C.c_int),
         "sm_multi_destroy": ([_vp], None),
         "sm_multi_spmv": ([_vp, _f32, _vp, _f32, _vp, C.c_int, _vp], C.c_int),
         "sm_multi_spmm": ([_vp, _i32, _f32, _vp, _f32, _vp, _i64, C.c_int, _vp], C.c_int),

@@ -83,6 +83,15 @@ void free_xband_dev(XbandDev &h) {
     h = XbandDev();
 }
 
+// The native-format plan (upload_native); left empty, as a matrix without one.
+void free_native_dev(NativeDev &n) {
+    for (void *p : {(void *)n.d_pos, (void *)n.d_val, (void *)n.d_beg, (void *)n.d_end, (void *)n.d_col,
+                    (void *)n.d_table, (void *)n.d_pbatch, (void *)n.d_bmeta, (void *)n.d_boff,
+                    (void *)n.d_lists, (void *)n.d_hdr})
+        (void)hipFree(p);
+    n = NativeDev{};
+}
+
 void free_device(sm_matrix *m) {
     DeviceGuard g(m->device);
     (void)hipFree(m->d_row_ptr);
@@ -103,16 +112,11 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.d_perm);
     (void)hipFree(m->plan.d_rcol);
     (void)hipFree(m->plan.d_xperm);
-    (void)hipFree(m->plan.sell.d_off);
-    (void)hipFree(m->plan.sell.d_len);
-    (void)hipFree(m->plan.sell.d_row);
-    (void)hipFree(m->plan.sell.d_row_len);
-    (void)hipFree(m->plan.sell.d_col);
-    (void)hipFree(m->plan.sell.d_val);
-    (void)hipFree(m->plan.sell.d_table);
-    (void)hipFree(m->plan.sell.d_long_rows);
-    (void)hipFree(m->plan.sell.d_long_ptr);
-    (void)hipFree(m->plan.sell.d_partials);
+    for (SellDev *d : {&m->plan.sell, &m->plan.xsell})
+        for (void *p : {(void *)d->d_off, (void *)d->d_len, (void *)d->d_row, (void *)d->d_row_len,
+                        (void *)d->d_col, (void *)d->d_val, (void *)d->d_table, (void *)d->d_long_rows,
+                        (void *)d->d_long_ptr, (void *)d->d_partials})
+            (void)hipFree(p);
     (void)hipFree(m->plan.cc.d_off);
     (void)hipFree(m->plan.cc.d_len);
     (void)hipFree(m->plan.cc.d_row);
@@ -120,20 +124,10 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.cc.d_word);
     (void)hipFree(m->plan.cc.d_val);
     (void)hipFree(m->plan.cc.d_table);
-    (void)hipFree(m->plan.nat.d_pos);
-    (void)hipFree(m->plan.nat.d_val);
-    (void)hipFree(m->plan.nat.d_beg);
-    (void)hipFree(m->plan.nat.d_end);
-    (void)hipFree(m->plan.nat.d_col);
-    (void)hipFree(m->plan.nat.d_table);
+    free_native_dev(m->plan.nat);
     (void)hipFree(m->plan.sw.d_block_chunk);
     (void)hipFree(m->plan.sw.d_ent);
     (void)hipFree(m->plan.sw.d_table);
-    (void)hipFree(m->plan.nat.d_pbatch);
-    (void)hipFree(m->plan.nat.d_bmeta);
-    (void)hipFree(m->plan.nat.d_boff);
-    (void)hipFree(m->plan.nat.d_lists);
-    (void)hipFree(m->plan.nat.d_hdr);
     free_xband_dev(m->plan.hot);
     (void)hipFree(m->d_ws);
     if (m->ws_ready) (void)hipEventDestroy(m->ws_ready);
@@ -188,6 +182,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.ccsell = d.ccsell;
         r.ccsell_chunk_log2 = d.ccsell_chunk_log2;
         r.hot_cols = d.hot_cols;
+        r.exact_sell = d.exact_sell;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -231,6 +226,7 @@ sm_status check_opts(const sm_build_opts *o) {
     if (r.ccsell_chunk_log2 != 0 && (r.ccsell_chunk_log2 < 8 || r.ccsell_chunk_log2 > 24))
         return fail(SM_ERR_INVALID_ARG, "ccsell_chunk_log2 must be 0 or 8..24");
     if (r.hot_cols < -1) return fail(SM_ERR_INVALID_ARG, "hot_cols must be -1, 0 or positive");
+    if (r.exact_sell < -1 || r.exact_sell > 1) return fail(SM_ERR_INVALID_ARG, "exact_sell must be -1, 0 or 1");
     return SM_OK;
 }
 
@@ -544,7 +540,8 @@ bool want_sell(const sm_matrix *m) {
 }
 
 sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
-                      int64_t nnz = -1, bool cols_relabeled = false) {
+                      int64_t nnz = -1, bool cols_relabeled = false, SellDev *target = nullptr,
+                      int32_t max_len_override = 0) {
     Plan &p = m->plan;
     if (nnz < 0) nnz = m->nnz;
     std::vector<int32_t> rcol;
@@ -556,7 +553,9 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     }
     // Rows up to max_len terms go to the slices (one lane each, in stored order); the
     // longer ones as max_len-term segments.  sell_max_len overrides the cap.
-    const int32_t max_len = m->opts.sell_max_len > 0 ? m->opts.sell_max_len : kSellMaxLen;
+    const int32_t max_len = max_len_override > 0       ? max_len_override
+                            : m->opts.sell_max_len > 0 ? m->opts.sell_max_len
+                                                       : kSellMaxLen;
     // sell_sigma: sort within windows of that many rows (0: one window),
     // sell_streams: XCD streams of windows (default 8 with windows).
     const int64_t sigma = std::max<int64_t>(0, m->opts.sell_sigma);
@@ -574,7 +573,7 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     std::vector<uint8_t>().swap(ids);
     if (sh.n_slices == 0) return SM_OK;
     if (sh.padded >= ((int64_t)1 << 31) - kSellLanes * kSellUnroll) return SM_OK;
-    SellDev &d = p.sell;
+    SellDev &d = target ? *target : p.sell;
     d.max_len = max_len;
     d.n_long = (int32_t)sh.long_rows.size();
     const int32_t n_parts = sh.long_ptr.back();
@@ -612,6 +611,38 @@ sm_status upload_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const
     }
     d.n_slices = sh.n_slices;
     return SM_OK;
+}
+
+// SM_ALGO_EXACT: the fastest launch built for `m` that adds every output's terms in the
+// reference's order (kernel.cc:780-796, sparse-matrix.cc:164-190) -- what the reference's
+// C++ surface runs (sblas_shim.cpp).  The band kernels need x 16-byte aligned (`x16`).
+// kAlgoExactSell: the unsegmented sliced ELL built for this (upload_exact_sell).
+constexpr int kAlgoExactSell = 100;
+
+int exact_algo(const sm_matrix *m, bool x16) {
+    const Plan &pl = m->plan;
+    if (pl.sw.n_blocks > 0) return SM_ALGO_XBAND;                                  // column-swept blocks
+    if (pl.xb.n_blocks > 0 && pl.xb.n_slabs == 1 && x16) return SM_ALGO_XBAND;    // one slab of bands
+    if (pl.cc.n_slices > 0) return SM_ALGO_SELL;                                    // column-chunked ELL
+    if (pl.sell.n_slices > 0 && pl.sell.n_long == 0 && pl.hot.n_blocks == 0) return SM_ALGO_SELL;
+    if (pl.max_row_nnz <= SM_SERIAL_ROW_MAX) return SM_ALGO_STREAM;                // serial rows only
+    if (pl.xsell.n_slices > 0) return kAlgoExactSell;
+    return SM_ALGO_PARITY;
+}
+
+// The unsegmented sliced ELL for SM_ALGO_EXACT (sm_build_opts.exact_sell): by default for
+// matrices made by the CopyForm constructors -- the reference's own path, whose C++
+// surface promises its results bit for bit -- when nothing else built keeps the order.
+bool want_exact_sell(const sm_matrix *m) {
+    if (m->nnz == 0 || m->n_rows == 0 || m->opts.exact_sell < 0) return false;
+    if (m->opts.exact_sell == 0 && !m->from_index) return false;
+    return exact_algo(m, true) == SM_ALGO_PARITY;
+}
+
+sm_status upload_exact_sell(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    // Rows never cut: the slice cap is the longest row (a lane walks its whole row).
+    const int32_t cap = std::max<int32_t>(m->plan.max_row_nnz, 1);
+    return upload_sell(m, rp, col, val, -1, false, &m->plan.xsell, cap);
 }
 
 // Column-chunked sorted sliced-ELL (ccsell.h, kernels_ccsell.hip):
@@ -934,6 +965,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     if (st2 == SM_OK && want_ccsell(m)) st2 = upload_ccsell(m, rp, col, val);
     if (st2 == SM_OK && want_sell(m)) st2 = upload_sell_layouts(m, rp, col, val);
+    if (st2 == SM_OK && want_exact_sell(m)) st2 = upload_exact_sell(m, rp, col, val);
     return st2;
 }
 
@@ -1050,6 +1082,7 @@ sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t
     m->s_rows = er.s_rows;
     m->s_cols = er.s_cols;
     m->has_ref = true;   // the reference encoding exists (possibly empty)
+    m->from_index = true;
     m->table_size = er.table_size;
     m->table = std::move(er.table);
     m->pos = std::move(er.pos);
@@ -1153,9 +1186,13 @@ sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows
                                tr ? d_rp : d_offs, d_table, d_col, d_val, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);   // host vectors above go out of scope
     if (e != hipSuccess) { cleanup(); return hip_fail(e, "dense index fill"); }
-    st = sm_create_from_csr_device(nb, kb, nnz, d_rp, d_col, d_val, device, stream, out);
+    sm_build_opts o;   // the CopyForm path: SM_ALGO_EXACT keeps a reference-order kernel
+    sm_build_opts_init(&o);
+    o.exact_sell = 1;
+    st = sm_create_from_csr_device_ex(nb, kb, nnz, d_rp, d_col, d_val, device, stream, &o, out);
     cleanup();
     if (st == SM_OK) {
+        (*out)->from_index = true;
         (*out)->table_size = table_size;
         (*out)->table = std::move(tb);
     }
@@ -1352,6 +1389,11 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->ccsell_chunks = m->plan.cc.n_slices > 0 ? m->plan.cc.n_chunks : 0;
     info->hot_cols = m->plan.hot.n_blocks > 0 ? m->plan.hot_cols : 0;
     info->sweep_blocks = (int32_t)std::min<int64_t>(m->plan.sw.n_blocks, INT32_MAX);
+    info->exact_sell_slices = m->plan.xsell.n_slices;
+    {
+        const int a = exact_algo(m, true);
+        info->exact_algo = a == kAlgoExactSell ? (int32_t)SM_ALGO_SELL : a;
+    }
     // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
     memcpy(out, &full, std::min(info_bytes, sizeof(full)));
     return SM_OK;
@@ -1400,7 +1442,19 @@ sm_status sm_build_ref_stream(sm_matrix *m, const float *table, int32_t table_si
     m->panel_begin = std::move(er.panel_begin);
     m->panel_end = std::move(er.panel_end);
     m->has_ref = true;
-    return upload_native(m);
+    st = upload_native(m);
+    if (st != SM_OK) {   // no half-built encoding -- a retry starts over
+        free_native_dev(m->plan.nat);
+        m->has_ref = false;
+        m->table_size = 0;
+        for (auto *v : {&m->pos, &m->val}) std::vector<uint8_t>().swap(*v);
+        std::vector<float>().swap(m->table);
+        std::vector<int32_t>().swap(m->panel_row_off);
+        std::vector<int32_t>().swap(m->panel_col_off);
+        std::vector<int64_t>().swap(m->panel_begin);
+        std::vector<int64_t>().swap(m->panel_end);
+    }
+    return st;
 }
 
 sm_status sm_copy_csr(const sm_matrix *m, int32_t *row_ptr, int32_t *col_idx, float *val) {
@@ -1460,6 +1514,7 @@ int32_t sm_equal(const sm_matrix *a, const sm_matrix *b) {
 }
 
 // ---------------------------------------------------------------------------
+
 sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, float *y,
                   sm_algo algo, sm_stream stream) {
     if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
@@ -1485,11 +1540,13 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         e = after_launch(e, s, "sm_spmv native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv native");
     }
-    if (algo < SM_ALGO_AUTO || algo > SM_ALGO_SELL) return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
+    const int ai = algo == SM_ALGO_EXACT ? exact_algo(m, ((uintptr_t)x % 16) == 0) : (int)algo;
+    if ((ai < SM_ALGO_AUTO || ai > SM_ALGO_SELL) && ai != kAlgoExactSell)
+        return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     // The matrix's SpMV scratch (sm_internal.h): SpMVs that use it run one after the
     // other on the device, whatever stream or thread issues them.
     const Plan &pl = m->plan;
-    const bool scratch = algo != SM_ALGO_PARITY && algo != SM_ALGO_VECTOR &&
+    const bool scratch = ai != SM_ALGO_PARITY && ai != SM_ALGO_VECTOR &&
                          ((pl.xb.n_blocks > 0 && pl.xb.n_slabs > 1) || pl.n_relabel > 0 ||
                           (pl.hot.n_blocks > 0 && pl.hot.n_slabs > 1) ||
                           pl.sell.n_long > 0 || pl.n_long > 0);
@@ -1505,7 +1562,7 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (ordered && e == hipSuccess && m->scratch_recorded) e = hipStreamWaitEvent(s, m->scratch_ready, 0);
         if (e != hipSuccess) return hip_fail(e, "sm_spmv scratch ordering");
     }
-    switch (algo) {
+    switch (ai) {
     case SM_ALGO_PARITY:
         e = launch_spmv_parity(n, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta, s);
         break;
@@ -1547,6 +1604,15 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
             break;
         }
         [[fallthrough]];   // no sell layout -> stream kernel
+    case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
+        const float *xs = x;
+        if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns
+            e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
+            xs = m->plan.d_xperm;
+        }
+        if (e == hipSuccess) e = launch_spmv_sell(m->plan.xsell, xs, y, alpha, beta, s);
+        break;
+    }
     case SM_ALGO_STREAM:
         // Long-row partial sums (and the relabeled x) live in the matrix (allocated at
         // creation): SpMVs on one matrix must not run concurrently on different streams.
@@ -1589,7 +1655,8 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     }
     const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
                         ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
-    if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND) algo = SM_ALGO_AUTO;   // SpMV layouts
+    if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND || algo == SM_ALGO_EXACT)
+        algo = SM_ALGO_AUTO;   // SpMV layouts; the SpMM kernels keep every row's order
     if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
         e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X,
                                  ldx, m->n_cols, Y, ldy, alpha, beta, algo != SM_ALGO_VECTOR, s);
@@ -1628,6 +1695,15 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
                   });
         e = after_launch(e, s, "sm_addmatmat native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat native");
+    }
+    if (algo != SM_ALGO_PARITY && m > 128 && k > 0) {
+        // Rows of A and C are independent products: row-panel calls of <= 128 rows each.
+        for (int32_t i0 = 0; i0 < m; i0 += 128) {
+            const sm_status st = sm_addmatmat(mat, a + (int64_t)i0 * lda, std::min<int32_t>(128, m - i0),
+                                              lda, c + (int64_t)i0 * ldc, ldc, alpha, beta, algo, stream);
+            if (st != SM_OK) return st;
+        }
+        return SM_OK;
     }
     if (algo != SM_ALGO_PARITY && m <= 128 && k > 0) {
         // C^T = B A^T through the row-panel SpMM (the reference transposes too,
@@ -1697,9 +1773,9 @@ sm_status sm_addmatmat_host(const sm_matrix *mat, const float *a, int32_t m, int
     if (e == hipSuccess) e = hipMemcpy(dc, c, (size_t)c_elems * 4, hipMemcpyHostToDevice);
     sm_status st = SM_OK;
     if (e == hipSuccess) {
-        // Bit-exact either way: m = 1 the parity SpMV, m > 1 the row-panel path.
-        st = sm_addmatmat(mat, da, m, lda, dc, ldc, alpha, beta,
-                          m == 1 ? SM_ALGO_PARITY : SM_ALGO_AUTO, nullptr);
+        // Bit-exact: the fastest reference-order kernels (SM_ALGO_EXACT: m = 1 a
+        // reference-order SpMV layout, else parity; m > 1 the row-panel path).
+        st = sm_addmatmat(mat, da, m, lda, dc, ldc, alpha, beta, SM_ALGO_EXACT, nullptr);
         if (st == SM_OK) e = hipMemcpy(c, dc, (size_t)c_elems * 4, hipMemcpyDeviceToHost);
     }
     (void)hipFree(da);

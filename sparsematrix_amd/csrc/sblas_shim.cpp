@@ -183,10 +183,19 @@ template <typename P, typename V, typename T, const int32 brs, const int32 bcs>
 void SparseMatrix<P, V, T, brs, bcs>::AddMatMat(T *a, int32 m, int32 lda, T *c, int32 ldc,
                                                  T alpha, T beta) {
     if (!handle_) return;
+    // SM_ALGO_EXACT: the fastest kernels the matrix holds that add every output's terms
+    // in the reference's order (sparse-matrix.cc:164-190, kernel.cc:780-796), so the
+    // result is the reference's bit for bit: m = 1 a reference-order SpMV layout (one
+    // slab of bands, sliced ELL without segments, ...), m > 1 the row-panel SpMM.
     if (is_device_ptr(c)) {
-        report(sm_addmatmat(handle_, a, m, lda, c, ldc, alpha, beta, SM_ALGO_PARITY, nullptr),
+        // Device C: queued on the legacy default stream and not waited for -- every later
+        // null-stream operation (hipMemcpy, a kernel on the default stream) sees the
+        // result, which is what "C is updated on return" means for device memory.  The
+        // reference is synchronous only because it is CPU code.  A host A is uploaded.
+        Staged<float> da(a, alpha != 0.0f ? span(m, lda, rows_) : 0);
+        if (!da.ok) { fprintf(stderr, "AddMatMat: staging A failed\n"); return; }
+        report(sm_addmatmat(handle_, da.dev, m, lda, c, ldc, alpha, beta, SM_ALGO_EXACT, nullptr),
                "AddMatMat");
-        report(sm_stream_sync(nullptr), "AddMatMat");
     } else {
         report(sm_addmatmat_host(handle_, a, m, lda, c, ldc, alpha, beta), "AddMatMat");
     }

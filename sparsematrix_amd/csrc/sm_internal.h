@@ -52,6 +52,7 @@ struct BuildOpts {
     int32_t ccsell = -1;
     int32_t ccsell_chunk_log2 = 0;
     int32_t hot_cols = 0;
+    int32_t exact_sell = 0;   // 0 auto, 1 always, -1 never (sm_build_opts.exact_sell)
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
@@ -165,6 +166,9 @@ struct SweepDev {   // column-swept row blocks (sweep.h)
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
+    // Unsegmented sorted sliced ELL (every row, any length, in the reference's order):
+    // SM_ALGO_EXACT's kernel when no other built layout keeps that order.
+    SellDev xsell;
     CcsellDev cc;                     // n_slices == 0 when not built
     NativeDev nat;                    // n_panels == 0 when not built (dense-index matrices)
     SweepDev sw;                      // n_blocks == 0 when not built
@@ -274,6 +278,7 @@ struct sm_matrix {
     int64_t device_bytes = 0;
     // Reference encoding (only for matrices built by sm_create_from_dense_index).
     bool has_ref = false;
+    bool from_index = false;   // built by the CopyForm constructors (the reference's path)
     int32_t table_size = 0;
     std::vector<float> table;                  // table_size + 1, last = 0
     std::vector<uint8_t> pos, val;

@@ -97,25 +97,92 @@ def partition_c(n_rows: int, world: int, rank: int) -> tuple[int, int]:
     return int(r0.value), int(r1.value)
 
 
+def host_staged_allgather(group=None):
+    """An all-gather for `MultiContext.with_collective` (sm_multi_create_with): the
+    rank's slice is copied to the host, gathered over `group` (any torch.distributed
+    backend -- gloo for a CPU control plane), and the gathered vector copied back.  It
+    synchronises the stream it is given and blocks until `recv` holds the result, as
+    the C ABI allows.  For ranks RCCL cannot serve (two ranks on one GPU) and for tests;
+    RCCL (MultiContext) is the production path."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    world = dist.get_world_size(group)
+
+    def allgather(send, recv, count, stream, user):
+        try:
+            if hip.hipStreamSynchronize(stream) != 0:
+                return 2
+            mine = torch.empty(count, dtype=torch.float32)
+            if count and hip.hipMemcpy(mine.data_ptr(), send, 4 * count, 2) != 0:   # D2H
+                return 3
+            full = torch.empty(count * world, dtype=torch.float32)
+            dist.all_gather_into_tensor(full, mine, group=group)
+            if count and hip.hipMemcpy(recv, full.data_ptr(), 4 * count * world, 1) != 0:   # H2D
+                return 4
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the C side as a failure
+            return 1
+    return allgather
+
+
 class MultiContext:
     """The C ABI's multi-GPU context (sm_multi_*, include/sparsematrix.h): one RCCL
     communicator over the ranks, one ncclAllGather of x per product, then the local
     SpMV.  `local` is this rank's rows of B with global columns (a SparseMatrix);
     `unique_id` the 128 bytes rank 0 made with MultiContext.unique_id() and handed to
-    every rank (bench.py broadcasts it over torch.distributed's gloo group)."""
+    every rank (bench.py broadcasts it over torch.distributed's gloo group).
+    `MultiContext.with_collective` builds the same context over a Python all-gather
+    instead of RCCL (sm_multi_create_with)."""
 
-    def __init__(self, local, nranks: int, rank: int, unique_id: bytes):
+    def __init__(self, local, nranks: int, rank: int, unique_id: bytes | None = None,
+                 collective=None):
         import ctypes as C
         from . import _lib
         self._L = _lib.load()
         self.local = local                       # the context refers to it: keep it alive
-        uid = _lib.SmUniqueId()
-        C.memmove(C.addressof(uid), bytes(unique_id), _lib.SM_UNIQUE_ID_BYTES)
         h = C.c_void_p()
-        _lib.check_multi(self._L.sm_multi_create(C.byref(uid), nranks, rank, local._require(),
-                                                 C.byref(h)), "sm_multi_create")
+        if collective is not None:
+            self._cb = _lib.SmAllgatherFn(collective)   # keep the trampoline alive
+            self._coll = _lib.SmCollective(self._cb, None)
+            _lib.check_multi(self._L.sm_multi_create_with(C.byref(self._coll), nranks, rank,
+                                                          local._require(), C.byref(h)),
+                             "sm_multi_create_with")
+        else:
+            uid = _lib.SmUniqueId()
+            C.memmove(C.addressof(uid), bytes(unique_id), _lib.SM_UNIQUE_ID_BYTES)
+            _lib.check_multi(self._L.sm_multi_create(C.byref(uid), nranks, rank, local._require(),
+                                                     C.byref(h)), "sm_multi_create")
         self._h = h
         self.nranks, self.rank = nranks, rank
+        info = local.info()
+        self.n_cols = int(info["n_cols"])
+        self.n_rows = int(info["n_rows"])
+        self.x_local_len = self.n_cols // nranks
+        self.device = int(info["device"])
+
+    @classmethod
+    def with_collective(cls, local, nranks: int, rank: int, allgather):
+        """The context over `allgather(send_ptr, recv_ptr, count, stream, user) -> int`
+        (e.g. host_staged_allgather(group)) instead of RCCL."""
+        return cls(local, nranks, rank, collective=allgather)
+
+    def _check(self, t, length: int, what: str, rows: int | None = None):
+        """The C side cannot check device buffers: dtype, layout, device and length."""
+        import torch
+        assert t.dtype == torch.float32, f"{what}: float32 expected, got {t.dtype}"
+        assert t.is_cuda and t.device.index == self.device, \
+            f"{what}: must be on cuda:{self.device}, got {t.device}"
+        if rows is None:
+            assert t.is_contiguous() and t.dim() == 1 and t.numel() == length, \
+                f"{what}: contiguous vector of {length} floats expected, got {tuple(t.shape)}"
+        else:
+            assert t.dim() == 2 and t.shape[0] == length and t.shape[1] == rows, \
+                f"{what}: ({length}, {rows}) expected, got {tuple(t.shape)}"
 
     @staticmethod
     def unique_id() -> bytes:
@@ -146,6 +213,8 @@ class MultiContext:
     def spmv(self, x_local, y_local, alpha=1.0, beta=1.0, algo="auto", stream=None):
         from . import _lib
         from .sparse_matrix import _algo
+        self._check(x_local, self.x_local_len, "x_local")
+        self._check(y_local, self.n_rows, "y_local")
         _lib.check_multi(self._L.sm_multi_spmv(self._h, alpha, x_local.data_ptr(), beta,
                                                y_local.data_ptr(), _algo(algo),
                                                self._stream(y_local, stream)), "sm_multi_spmv")
@@ -155,7 +224,10 @@ class MultiContext:
         from . import _lib
         from .sparse_matrix import _algo
         n_rhs = int(Y_local.shape[1])
-        assert X_local.is_contiguous() and X_local.shape[1] == n_rhs
+        self._check(X_local, self.x_local_len, "X_local", rows=n_rhs)
+        assert X_local.is_contiguous(), "X_local: contiguous rows expected"
+        self._check(Y_local, self.n_rows, "Y_local", rows=n_rhs)
+        assert Y_local.stride(1) == 1, "Y_local: rows must be contiguous"
         _lib.check_multi(self._L.sm_multi_spmm(self._h, n_rhs, alpha, X_local.data_ptr(), beta,
                                                Y_local.data_ptr(), int(Y_local.stride(0)),
                                                _algo(algo), self._stream(Y_local, stream)),
@@ -169,6 +241,13 @@ class MultiContext:
         from . import _lib
         from .sparse_matrix import _algo
         n = len(xs)
+        assert len(ys) == n and (mats is None or len(mats) == n), "one x, y (and matrix) per product"
+        for i in range(n):
+            self._check(xs[i], self.x_local_len, f"xs[{i}]")
+            rows = self.n_rows if mats is None else int(mats[i].info()["n_rows"])
+            assert ys[i].dtype.is_floating_point and ys[i].numel() == rows and ys[i].is_contiguous(), \
+                f"ys[{i}]: contiguous vector of {rows} floats expected"
+            self._check(ys[i], rows, f"ys[{i}]")
         xa = (C.c_void_p * n)(*[x.data_ptr() for x in xs])
         ya = (C.c_void_p * n)(*[y.data_ptr() for y in ys])
         ma = (C.c_void_p * n)(*[m._require().value for m in mats]) if mats is not None else None
@@ -179,6 +258,7 @@ class MultiContext:
     def allgather(self, x_local, n_rhs: int = 1, stream=None) -> int:
         import ctypes as C
         from . import _lib
+        self._check(x_local.reshape(-1), self.x_local_len * n_rhs, "x_local")
         p = C.c_void_p()
         _lib.check_multi(self._L.sm_multi_allgather(self._h, x_local.data_ptr(), n_rhs,
                                                     self._stream(x_local, stream), C.byref(p)),

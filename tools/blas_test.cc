@@ -17,13 +17,21 @@
 //                         reference-exact parity path, transfers included)
 //   sgemm_sparse_device   the same product with A and C resident on the GPU (fast
 //                         kernels; the time covers the kernels only)
+//   sm_addmatmat_auto     the C ABI's sm_addmatmat with SM_ALGO_AUTO on the same
+//                         device buffers (the library's own speed, for comparison:
+//                         the C++ surface runs SM_ALGO_EXACT, the reference's order)
 //   cpu_sgemm_baseline    the dense CPU product used as the checker (the reference
 //                         uses OpenBLAS cblas_sgemm, absent from this image)
+//
+// Timing: one call, as the reference's harness does (its repeat loop is commented out,
+// blas_test.h:199).  SBLAS_REPS=r > 1: one untimed call first, then the median of r
+// timed calls (each on fresh copies of C).
 //
 // Unlike the reference (srand(time)), the generator is seeded (SBLAS_SEED, default
 // 1) so a run can be repeated.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -36,6 +44,7 @@
 #include <vector>
 
 #include "sparse-matrix.h"
+#include "sparsematrix.h"   // the C ABI (sm_addmatmat AUTO row)
 
 namespace {
 
@@ -171,6 +180,25 @@ double now_ms() {
 
 }  // namespace
 
+// Median over `reps` runs of fn() (one untimed run first when reps > 1).
+template <class F>
+double timed_ms(int reps, F &&fn) {
+    if (reps <= 1) {
+        const double t0 = now_ms();
+        fn();
+        return now_ms() - t0;
+    }
+    fn();
+    std::vector<double> t;
+    for (int r = 0; r < reps; ++r) {
+        const double t0 = now_ms();
+        fn();
+        t.push_back(now_ms() - t0);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
 int main(int argc, char **argv) {
     Range rm(argc > 1 ? argv[1] : "117"), rn(argc > 2 ? argv[2] : "1023"),
         rk(argc > 3 ? argv[3] : "2047");
@@ -178,6 +206,8 @@ int main(int argc, char **argv) {
     const Filter filter(argc > 5 ? argv[5] : nullptr);
     const char *seed = getenv("SBLAS_SEED");
     g_rng.seed(seed ? (unsigned)atoi(seed) : 1u);
+    const char *reps_env = getenv("SBLAS_REPS");
+    const int reps = reps_env ? std::max(1, atoi(reps_env)) : 1;
     const float alpha = 1.0f, beta = 1.0f;   // the reference's sparse invoker (blas_test.h:307)
     Table table;
     int failures = 0;
@@ -201,27 +231,53 @@ int main(int argc, char **argv) {
                 }
                 if (filter.Match("sgemm_sparse")) {
                     std::vector<float> Ah = A, C = C0;
-                    const double t0 = now_ms();
-                    B.AddMatMat(Ah.data(), m, k, C.data(), n, alpha, beta);
-                    table.Add("sgemm_sparse", m, n, k, now_ms() - t0);
+                    const double ms = timed_ms(reps, [&] {
+                        C = C0;
+                        B.AddMatMat(Ah.data(), m, k, C.data(), n, alpha, beta);
+                    });
+                    table.Add("sgemm_sparse", m, n, k, ms);
                     if (do_check && !check("sgemm_sparse", C, want)) ++failures;
                 }
-                if (filter.Match("sgemm_sparse_device")) {
-                    float *dA = nullptr, *dC = nullptr;
+                const bool dev_fn = filter.Match("sgemm_sparse_device");
+                const bool auto_fn = filter.Match("sm_addmatmat_auto");
+                if (dev_fn || auto_fn) {
+                    float *dA = nullptr, *dC = nullptr, *dC0 = nullptr;
                     HIP_OK(hipMalloc((void **)&dA, A.size() * sizeof(float)));
                     HIP_OK(hipMalloc((void **)&dC, C0.size() * sizeof(float)));
+                    HIP_OK(hipMalloc((void **)&dC0, C0.size() * sizeof(float)));
                     HIP_OK(hipMemcpy(dA, A.data(), A.size() * 4, hipMemcpyHostToDevice));
-                    HIP_OK(hipMemcpy(dC, C0.data(), C0.size() * 4, hipMemcpyHostToDevice));
-                    HIP_OK(hipDeviceSynchronize());
-                    const double t0 = now_ms();
-                    B.AddMatMat(dA, m, k, dC, n, alpha, beta);
-                    HIP_OK(hipDeviceSynchronize());
-                    table.Add("sgemm_sparse_device", m, n, k, now_ms() - t0);
-                    std::vector<float> C(C0.size());
-                    HIP_OK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
+                    HIP_OK(hipMemcpy(dC0, C0.data(), C0.size() * 4, hipMemcpyHostToDevice));
+                    // Kernel time: C reset outside the timed call, device drained after it.
+                    auto run = [&](const char *name, auto &&call) {
+                        std::vector<double> t;
+                        for (int r = 0; r < (reps > 1 ? reps + 1 : 1); ++r) {
+                            HIP_OK(hipMemcpy(dC, dC0, C0.size() * 4, hipMemcpyDeviceToDevice));
+                            HIP_OK(hipDeviceSynchronize());
+                            const double t0 = now_ms();
+                            call();
+                            HIP_OK(hipDeviceSynchronize());
+                            if (reps <= 1 || r > 0) t.push_back(now_ms() - t0);
+                        }
+                        std::sort(t.begin(), t.end());
+                        table.Add(name, m, n, k, t[t.size() / 2]);
+                        std::vector<float> C(C0.size());
+                        HIP_OK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
+                        if (do_check && !check(name, C, want)) ++failures;
+                    };
+                    if (dev_fn)
+                        run("sgemm_sparse_device", [&] { B.AddMatMat(dA, m, k, dC, n, alpha, beta); });
+                    if (auto_fn)
+                        run("sm_addmatmat_auto", [&] {
+                            const sm_status st = sm_addmatmat(B.handle(), dA, m, k, dC, n, alpha, beta,
+                                                              SM_ALGO_AUTO, nullptr);
+                            if (st != SM_OK) {
+                                fprintf(stderr, "sm_addmatmat: %s\n", sm_last_error());
+                                exit(2);
+                            }
+                        });
                     HIP_OK(hipFree(dA));
                     HIP_OK(hipFree(dC));
-                    if (do_check && !check("sgemm_sparse_device", C, want)) ++failures;
+                    HIP_OK(hipFree(dC0));
                 }
             }
     table.Print();
