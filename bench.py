@@ -102,7 +102,7 @@ def available_cores() -> dict:
     return {"use": use, "affinity": aff, "cgroup_quota": quota, "nproc": os.cpu_count()}
 
 
-LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband"}
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband", 6: "gcb"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "sell": "spmv_sell_kernel / spmv_csell_kernel (sorted sliced-ELL)",
            "exact": "spmv_xband_kernel (exact band layout)",
@@ -112,6 +112,7 @@ KERNELS = {"stream": "spmv_stream_kernel",
            "cband": "spmv_band2_kernel<CB> (balanced bands of 4-byte codebook words, "
                     "distributed slab combine)",
            "ccsell": "spmv_ccsell_kernel (column-chunked sorted sliced-ELL)",
+           "gcb": "spmv_gcb_kernel (gathered chunk bands: 2016-term bands, x gathered, rows' sums in LDS)",
            "sweep": "spmv_sweep_kernel (column-swept 256-row blocks, one wavefront each)"}
 
 
@@ -157,6 +158,20 @@ def event_times(torch, fn, count: int) -> list:
     return [a.elapsed_time(b) for a, b in ev]
 
 
+def launch_ranks(n: int) -> int:
+    """torch.distributed.run with N local ranks on this very command line (a child
+    process; nothing in this process has initialised the GPU)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    return subprocess.call(cmd + sys.argv[1:])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +185,8 @@ def main():
     ap.add_argument("--replays", type=int, default=10,
                     help="N=1: extra graph replays for the per-SpMV time distribution")
     ap.add_argument("--algo", default="auto")
+    ap.add_argument("--layout", default="auto",
+                    help="A/B: force the matrix layout (sm_build_opts.layout name, e.g. gcb, gather)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
@@ -186,7 +203,18 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="N>1: all-gather then SpMV per step, instead of the all-gather of "
                          "step k+1 in flight beside the SpMV of step k")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the config-5 sub-line (2^26 x 2^26 strong scaling over the N ranks)")
+    ap.add_argument("--c5-global-rows", type=int, default=1 << 26)
+    ap.add_argument("--c5-steps", type=int, default=10)
+    ap.add_argument("--no-fp32-values", action="store_true",
+                    help="skip roofline.fp32_values (config 2 with arbitrary fp32 values)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` outside a launcher: start the N ranks ourselves (one
+        # process per GPU) before anything here touches the GPU, and exit with their code.
+        raise SystemExit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -234,7 +262,8 @@ def main():
     for k in range(replicas):
         seed = seed0 + 1000 * k + 7919 * rank
         rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
-        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index)
+        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index,
+                                      opts=None if args.layout == "auto" else dict(layout=args.layout))
         g = torch.Generator(device=dev).manual_seed(seed + 1)
         x_local = torch.rand(C // world if world > 1 else R, generator=g, device=dev) * 2 - 1
         x_full = (None if world > 1 else
@@ -267,8 +296,12 @@ def main():
             except Exception as exc:  # noqa: BLE001
                 err = exc
         dist.broadcast(uid, 0)
-        if rehearse:
-            err = RuntimeError("rehearsal: every rank on one GPU")
+        if rehearse:   # RCCL cannot put two ranks on one GPU: the same C-ABI context over gloo
+            from sparsematrix_amd.distributed import host_staged_allgather
+            try:
+                ctx = MultiContext.with_collective(reps[0]["M"], world, rank, host_staged_allgather())
+            except Exception as exc:  # noqa: BLE001
+                err = exc
         elif err is None and int(uid.sum()) != 0:
             try:
                 ctx = MultiContext(reps[0]["M"], world, rank, bytes(uid.numpy().tobytes()))
@@ -277,8 +310,9 @@ def main():
         ok = torch.tensor([1 if ctx is not None else 0], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if int(ok.item()) == 1:
-            path = "sm_multi_spmv_batch (C ABI, ncclAllGather)" if not args.no_overlap \
-                else "sm_multi_spmv (C ABI, ncclAllGather)"
+            coll = "host-staged gloo all-gather (rehearsal)" if rehearse else "ncclAllGather"
+            path = f"sm_multi_spmv_batch (C ABI, {coll})" if not args.no_overlap \
+                else f"sm_multi_spmv (C ABI, {coll})"
         else:
             # The C-ABI context failed on some rank: the same data path through torch's
             # RCCL group (all_gather_into_tensor + the local SpMV), reported as such.
@@ -502,6 +536,30 @@ def main():
         except Exception as exc:  # noqa: BLE001
             rmat = {"error": f"{type(exc).__name__}: {exc}"[:300]}
 
+    # ---- config 2 with arbitrary fp32 values (rank 0, N = 1) ------------------------
+    if (world == 1 and emu == 1 and args.workload == "config2" and not args.no_fp32_values
+            and reps[0]["rp"] is not None):
+        try:
+            roof["fp32_values"] = fp32_values_line(args, torch, reps, R, C, bytes_rank, dev, dev_index)
+        except Exception as exc:  # noqa: BLE001
+            roof["fp32_values"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
+    # ---- config 5: 2^26 x 2^26 strong scaling over the job's ranks ------------------
+    config5 = None
+    if args.workload == "config2" and emu == 1 and not args.no_config5:
+        if ctx is not None:   # the config-2 products are done with: make room
+            ctx.close()
+            ctx = None
+        for r in reps:
+            r["M"] = None
+        torch.cuda.empty_cache()
+        try:
+            config5 = config5_line(args, torch, dist, world, rank, dev, dev_index, rehearse)
+        except Exception as exc:  # noqa: BLE001
+            config5 = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+            if world > 1:
+                raise
+
     # ---- CPU baseline (rank 0, N = 1) --------------------------------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu and reps[0]["rp"] is not None:
@@ -522,7 +580,7 @@ def main():
                            f", {path}" + (": all-gather of step k+1 beside SpMV k"
                                           if overlap else "") if world > 1 else ""),
                        **({"emulate_world": emu} if emu > 1 else {})},
-            "roofline": roof, "cpu_baseline": cpu, "spmm": spmm, "rmat": rmat,
+            "roofline": roof, "cpu_baseline": cpu, "spmm": spmm, "rmat": rmat, "config5": config5,
         }
         print(json.dumps(line), flush=True)
     if ctx is not None:
@@ -530,6 +588,146 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def fp32_values_line(args, torch, reps, R, C, bytes_rank, dev, dev_index) -> dict:
+    """the headline's matrix with arbitrary fp32 values (no 255-entry
+    codebook: AUTO takes the 8-byte band2 entries instead of cband's 4-byte words), two
+    replicas of the same structure, the K SpMVs replayed as one graph like the headline."""
+    import sparsematrix_amd as smd
+    r0 = reps[0]
+    mats = []
+    for k in range(2):
+        g = torch.Generator(device=dev).manual_seed(77 + k)
+        va = torch.rand(r0["ci"].numel(), generator=g, device=dev) * 2 - 1
+        mats.append((smd.SparseMatrix.from_csr(r0["rp"], r0["ci"], va, C, device=dev_index),
+                     reps[k % len(reps)]["x_full"], torch.empty_like(reps[k % len(reps)]["y"]).uniform_(-1, 1)))
+        del va
+    info = mats[0][0].info()
+    steps = args.steps
+
+    def run():
+        for j in range(steps):
+            M, x, y = mats[j % 2]
+            M.spmv(x, y, 1.0, 0.5)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        run()
+    torch.cuda.synchronize()
+    per = []
+    for _ in range(max(3, args.replays)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        graph.replay()
+        b.record()
+        torch.cuda.synchronize()
+        per.append(a.elapsed_time(b) / steps)
+    ms = float(np.median(per))
+    ach = bytes_rank / (ms * 1e-3) / 1e9
+    del graph, mats
+    torch.cuda.empty_cache()
+    return {"layout": layout_of(info), "kernel": KERNELS.get(layout_of(info)), "kernel_ms": round(ms, 5),
+            "ms_stats": stats(per), "achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4),
+            "sample": "config 2's structure, values uniform fp32 (16.7 M distinct), 2 replicas, "
+                      "median over graph replays of the K SpMVs"}
+
+
+def config5_line(args, torch, dist, world, rank, dev, dev_index, rehearse) -> dict:
+    """SURVEY §8(d) config 5 (BASELINE.json configs[4]): the 2^26 x 2^26 matrix, 16 distinct
+    uniform columns per row (seed 5 + 7919 * rank per slice), row-split over the job's N
+    ranks -- strong scaling.  One RCCL all-gather of x per product through the C ABI
+    (sm_multi_spmv_batch; N = 1: the plain SpMV of the whole matrix), K products timed
+    between barriers, max over ranks.  Bytes: 8 nnz + 4 (rows + N) + N * 4 cols
+    + 8 rows summed over ranks, each rank reading all of x; frac = bytes / t / (N * 8 TB/s).
+    Also per rank: the local SpMV alone (events, max over ranks of the medians) and the
+    all-gather alone."""
+    import sparsematrix_amd as smd
+    from sparsematrix_amd import synth
+    from sparsematrix_amd.distributed import MultiContext, host_staged_allgather
+    C, per = args.c5_global_rows, args.per_row
+    if C % world:
+        return {"error": f"{C} rows do not split over {world} ranks"}
+    R = C // world
+    t_b = time.perf_counter()
+    rp, ci, va = synth.uniform_rows_device(R, C, per, seed=5 + 7919 * rank, device=dev)
+    M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index,
+                                  opts=None if args.layout == "auto" else dict(layout=args.layout))
+    del rp, ci, va
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_b
+    g = torch.Generator(device=dev).manual_seed(6 + rank)
+    x_local = torch.rand(C // world, generator=g, device=dev) * 2 - 1
+    y = torch.rand(R, generator=g, device=dev) * 2 - 1
+    x_full = torch.rand(C, generator=g, device=dev) * 2 - 1
+    ctx = None
+    if world > 1:
+        if rehearse:
+            ctx = MultiContext.with_collective(M, world, rank, host_staged_allgather())
+        else:
+            uid = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                uid = torch.frombuffer(bytearray(MultiContext.unique_id()), dtype=torch.uint8).clone()
+            dist.broadcast(uid, 0)
+            ctx = MultiContext(M, world, rank, bytes(uid.numpy().tobytes()))
+    K = max(1, args.c5_steps)
+
+    def run(count):
+        if ctx is None:
+            for _ in range(count):
+                M.spmv(x_full, y, 1.0, 0.5)
+        else:
+            ctx.spmv_batch([x_local] * count, [y] * count, 1.0, 0.5)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+    run(2)
+    barrier()
+    t0 = time.perf_counter()
+    run(K)
+    barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    local = event_times(torch, lambda i: M.spmv(x_full, y, 1.0, 0.5), K)
+    lm = torch.tensor([float(np.median(local))], dtype=torch.float64)
+    ag = (event_times(torch, lambda i: ctx.allgather(x_local), K) if ctx is not None else None)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lm, op=dist.ReduceOp.MAX)
+    step_ms = 1e3 * float(el.item()) / K
+    nnz = C * per
+    bytes_total = 8 * nnz + 4 * (C + world) + world * 4 * C + 8 * C
+    bytes_rank = 8 * R * per + 4 * (R + 1) + 4 * C + 8 * R
+    value = bytes_total / (step_ms * 1e-3) / 1e9
+    info = M.info()
+    lay = layout_of(info)
+    wl = f"config5_{C}x{C}_{per}_per_row_rank0of{world}"
+    traffic = load_traffic(wl, lay)
+    lms = float(lm.item())
+    out = {"workload": f"config5_{C}x{C}_{per}_per_row", "ranks": world, "rows_per_rank": R,
+           "scaling": "strong", "steps": K, "ms_per_step": round(step_ms, 4),
+           "value": round(value, 1), "unit": "GB/s", "frac": round(value / (world * PEAK_HBM_GBS), 4),
+           "alg_bytes_total": bytes_total, "alg_bytes_rank": bytes_rank,
+           "local_spmv_ms_max_over_ranks": round(lms, 4), "local_spmv_ms_rank0": stats(local),
+           "kernel_frac": round(bytes_rank / (lms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+           "layout": lay, "kernel": KERNELS.get(lay, lay), "build_s": round(build_s, 1),
+           "traffic": traffic,
+           "traffic_source": (f"profiles/traffic_{wl}_{lay}.json (rocprofv3 PMC)" if traffic else None),
+           "path": ("one SpMV of the whole matrix per step" if ctx is None else
+                    "sm_multi_spmv_batch: one all-gather of x per product (C ABI, "
+                    + ("host-staged gloo" if rehearse else "ncclAllGather")
+                    + "), all-gather k+1 beside SpMV k")}
+    if ag is not None:
+        out["allgather_ms"] = stats(ag)
+        out["allgather_bytes_per_rank"] = 4 * C
+    if ctx is not None:
+        ctx.close()
+    del M, x_local, x_full, y
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(args, r0, bytes_rank, rmat_host):

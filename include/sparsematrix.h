@@ -83,13 +83,19 @@ typedef enum sm_algo {
                              panels) decoded on the device; bit-identical for every
                              output; only for matrices built from the dense index
                              (SM_ERR_NOT_SUPPORTED otherwise)                          */
-    SM_ALGO_EXACT = 7     /* the fastest kernel built for the matrix that adds every
+    SM_ALGO_EXACT = 7,    /* the fastest kernel built for the matrix that adds every
                              output's terms in the reference's order (bit-identical):
                              the column-swept or one-slab band layout, the column-chunked
                              or segment-free sliced ELL, the stream kernel when no row
                              exceeds SM_SERIAL_ROW_MAX terms, else PARITY.  SpMM and
                              AddMatMat with m > 1: the row-panel kernels (every row in
                              order).  What the reference's C++ surface (libsblas) runs. */
+    SM_ALGO_MFMA = 8      /* SpMM with n_rhs == 32 only: 16-row tiles on the matrix cores
+                             (v_mfma_f32_16x16x4_f32, four terms per step), one fused
+                             multiply-add per term: within the sum|terms| bound, not
+                             bit-identical; X must be finite (a non-finite X row makes
+                             the tile's other outputs NaN).  SM_ERR_NOT_SUPPORTED for
+                             other shapes and for SpMV.                                */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the
@@ -113,8 +119,9 @@ typedef struct sm_info {
     int32_t max_row_nnz;        /* longest row                                 */
     int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
                                    2 blocked, 3 gather, 4 band2 (balanced bands),
-                                   5 cband (balanced bands, codebook words);
-                                   2-5 sum each column slab in the reference's
+                                   5 cband (balanced bands, codebook words),
+                                   6 gcb (gathered chunk bands);
+                                   2-6 sum each column slab in the reference's
                                    order and add the slab sums in slab order     */
     int32_t xband_blocks, xband_bands;
     int32_t xband_slabs;        /* column slabs per row block (1: bit-identical) */
@@ -199,8 +206,11 @@ typedef enum sm_layout {
     SM_LAYOUT_NO_BANDS = 6,  /* no band layout: sorted sliced-ELL, else the stream kernel   */
     SM_LAYOUT_BANDS = 7,     /* a band layout even where the cost model would decline; the
                                 kind as AUTO would pick it                                */
-    SM_LAYOUT_SWEEP = 8      /* column-swept row blocks (wide matrices, <= 255 values): one
+    SM_LAYOUT_SWEEP = 8,     /* column-swept row blocks (wide matrices, <= 255 values): one
                                 wavefront per 256 rows, terms in column order, no barrier  */
+    SM_LAYOUT_GCB = 9        /* gathered chunk bands (wide matrices, x far beyond L2): 32K-row
+                                tiles, bands of up to 2016 terms within 2^18 columns, x
+                                gathered per term, rows' sums in LDS                      */
 } sm_layout;
 
 typedef struct sm_build_opts {

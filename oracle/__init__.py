@@ -72,6 +72,8 @@ def lib():
                                          C.c_float, C.c_int32]
         L.om_csr_spmm.argtypes = [C.c_int64, _i64p, _i32p, _f32p, C.c_int32, _f32p, C.c_int64,
                                   _f32p, C.c_int64, C.c_float, C.c_float]
+        L.om_csr_spmm_fma.argtypes = [C.c_int64, _i64p, _i32p, _f32p, C.c_int32, _f32p, C.c_int64,
+                                  _f32p, C.c_int64, C.c_float, C.c_float]
         L.om_csr_spmv_f64.argtypes = [C.c_int64, _i64p, _i32p, _f32p, _f32p, _f32p, _f64p, _f64p,
                                       C.c_float, C.c_float]
         L.om_beta.argtypes = [_f32p, C.c_int32, C.c_int32, C.c_int32, C.c_float]
@@ -211,6 +213,18 @@ def csr_spmm(row_ptr, col_idx, val, X, Y, alpha=1.0, beta=1.0) -> np.ndarray:
     lib().om_csr_spmm(n, np.ascontiguousarray(row_ptr, np.int64), _nz1(col_idx, np.int32),
                       _nz1(val, np.float32), N, _nz1(X, np.float32), N, out.reshape(-1),
                       N, alpha, beta)
+    return out
+
+
+def csr_spmm_fma(row_ptr, col_idx, val, X, Y, alpha=1.0, beta=1.0) -> np.ndarray:
+    """NOT the reference: the fma-chain model of SM_ALGO_MFMA (refmodel.c om_csr_spmm_fma)."""
+    X = np.ascontiguousarray(X, np.float32)
+    out = np.array(Y, np.float32, copy=True)
+    n, N = out.shape
+    if n == 0 or N == 0:
+        return out
+    lib().om_csr_spmm_fma(n, np.ascontiguousarray(row_ptr, np.int64), _nz1(col_idx, np.int32),
+                          _nz1(val, np.float32), N, X, X.shape[1], out, N, alpha, beta)
     return out
 
 

@@ -72,6 +72,10 @@ void om_csr_spmv(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
 void om_csr_spmm(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
                  const float *val, int32_t n_rhs, const float *X, int64_t ldx,
                  float *Y, int64_t ldy, float alpha, float beta);
+/* Not the reference: the fma-chain model of SM_ALGO_MFMA (tests only). */
+void om_csr_spmm_fma(int64_t n_rows, const int64_t *row_ptr, const int32_t *col_idx,
+                 const float *val, int32_t n_rhs, const float *X, int64_t ldx,
+                 float *Y, int64_t ldy, float alpha, float beta);
 
 /* Same as om_csr_spmv but with int32 row_ptr (the device format). */
 void om_csr_spmv_i32(int64_t n_rows, const int32_t *row_ptr, const int32_t *col_idx,

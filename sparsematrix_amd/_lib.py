@@ -32,7 +32,7 @@ SM_ERR_NO_DEVICE = 7
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
 ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5, "native": 6,
-         "exact": 7}
+         "exact": 7, "mfma": 8}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (
@@ -81,7 +81,7 @@ class SmInfo(C.Structure):
 
 # sm_layout
 LAYOUTS = {"auto": 0, "exact": 1, "blocked": 2, "gather": 3, "band2": 4, "cband": 5,
-           "no_bands": 6, "bands": 7, "sweep": 8}
+           "no_bands": 6, "bands": 7, "sweep": 8, "gcb": 9}
 
 
 class SmBuildOpts(C.Structure):

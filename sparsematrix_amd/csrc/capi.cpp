@@ -17,6 +17,7 @@
 #include "ccsell.h"
 #include "sweep.h"
 #include "encode.h"
+#include "gcb.h"
 #include "sm_internal.h"
 #include "sell.h"
 #include "xband.h"
@@ -190,6 +191,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         for (int k = 1; k <= 5; ++k)
             if (strcmp(e, names[k]) == 0) r.layout = k;
         if (strcmp(e, "sweep") == 0) r.layout = SM_LAYOUT_SWEEP;
+        if (strcmp(e, "gcb") == 0) r.layout = SM_LAYOUT_GCB;
     }
     if (const char *e = dev_env("SM_BAND_TALL")) r.band_tall = atoi(e);
     if (const char *e = dev_env("SM_BAND2_SLABS")) r.band_slabs = atoi(e);
@@ -213,7 +215,7 @@ sm_status check_opts(const sm_build_opts *o) {
         return fail(SM_ERR_INVALID_ARG, "sm_build_opts.struct_size %d: call sm_build_opts_init",
                     o->struct_size);
     const BuildOpts r = resolve_opts(o);
-    if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_SWEEP)
+    if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_GCB)
         return fail(SM_ERR_INVALID_ARG, "unknown layout %d", r.layout);
     if (r.band_slabs < 0 || r.band_slabs > 16) return fail(SM_ERR_INVALID_ARG, "band_slabs not in [0, 16]");
     if (r.gather_band_log2 != 0 && (r.gather_band_log2 < 13 || r.gather_band_log2 > 15))
@@ -236,7 +238,8 @@ int32_t tile_nnz_setting(const sm_matrix *m) {
 }
 
 bool kind_forced(const sm_matrix *m) {
-    return m->opts.layout >= SM_LAYOUT_EXACT && m->opts.layout <= SM_LAYOUT_CBAND;
+    return (m->opts.layout >= SM_LAYOUT_EXACT && m->opts.layout <= SM_LAYOUT_CBAND) ||
+           m->opts.layout == SM_LAYOUT_GCB;
 }
 
 // Column-band layout.  SM_LAYOUT_NO_BANDS disables it,
@@ -261,6 +264,7 @@ XbKind xband_kind_setting(const sm_matrix *m) {
     case SM_LAYOUT_GATHER: return kXbGather;
     case SM_LAYOUT_BAND2: return kXbBand2;
     case SM_LAYOUT_CBAND: return kXbCband;
+    case SM_LAYOUT_GCB: return kXbGcb;
     default: break;
     }
     return m->n_cols > kGatherCols ? kXbGather : kXbCband;
@@ -397,8 +401,49 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
                        m->opts.band_tall, m->opts.band_slabs, kind_forced(m));
 }
 
+// Gathered chunk bands (gcb.h, kernels_gcb.hip): 32K-row tiles where the rows make at
+// least 256 of them (one per CU), else 16K-row tiles; slabs so the tiles reach 256.
+static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    const int rows_log2 = m->n_rows >= ((int64_t)kXbTargetTiles << 15) ? 15 : 14;
+    const int64_t nblk = (m->n_rows + ((int64_t)1 << rows_log2) - 1) >> rows_log2;
+    int32_t slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
+    if (m->opts.band_slabs > 0) slabs = m->opts.band_slabs;
+    GcbHost gh;
+    if (!gcb_build(rp, col, val, m->n_rows, m->n_cols, rows_log2, slabs, kGcbMaxWindow, gh)) return SM_OK;
+    XbandDev &d = m->plan.xb;
+    const int64_t ntile = (int64_t)gh.n_blocks * gh.n_slabs;
+    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, gh.n_bands), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, gh.n_bands * kGcbBandWords), m->device_bytes));
+    if (gh.n_slabs > 1) {
+        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
+        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(gh.n_slabs - 1) * ps, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)gh.n_blocks, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)gh.n_blocks * 4 * sizeof(int32_t)));
+    }
+    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, gh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
+                         hipMemcpyHostToDevice));
+    if (gh.n_bands > 0) {
+        SM_TRY_HIP(hipMemcpy(d.d_band_clo, gh.band_clo.data(), (size_t)gh.n_bands * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_word, gh.ent.data(), (size_t)gh.n_bands * kGcbBandWords * 4,
+                             hipMemcpyHostToDevice));
+    }
+    d.kind = kXbGcb;
+    d.threads = 1024;
+    d.block_rows = gh.block_rows;
+    d.band_cols = gh.window;
+    d.n_bands = (int32_t)std::min<int64_t>(gh.n_bands, INT32_MAX);
+    d.n_slabs = gh.n_slabs;
+    d.slab_bands = gh.slab_cols;
+    d.n_chunks = gh.n_bands * kGcbChunks;
+    d.max_chunks_per_band = gh.max_bands_per_tile;
+    d.n_blocks = gh.n_blocks;
+    return SM_OK;
+}
+
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
                        XbKind kind) {
+    if (kind == kXbGcb) return upload_gcb(m, rp, col, val);
     if (kind == kXbBand2 || kind == kXbCband) {
         const sm_status st = upload_band2(m, rp, col, val, kind);
         if (st == SM_OK && m->plan.xb.n_blocks == 0 && !kind_forced(m))
@@ -1540,6 +1585,7 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         e = after_launch(e, s, "sm_spmv native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmv native");
     }
+    if (algo == SM_ALGO_MFMA) return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_MFMA is an SpMM algorithm (n_rhs = 32)");
     const int ai = algo == SM_ALGO_EXACT ? exact_algo(m, ((uintptr_t)x % 16) == 0) : (int)algo;
     if ((ai < SM_ALGO_AUTO || ai > SM_ALGO_SELL) && ai != kAlgoExactSell)
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
@@ -1579,6 +1625,8 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
             e = m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
                     ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
+                : m->plan.xb.kind == kXbGcb
+                    ? launch_spmv_gcb(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                     : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);
             break;
         }
@@ -1652,6 +1700,16 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     if (alpha == 0.0f) {
         e = beta != 1.0f ? launch_beta(Y, n, n_rhs, ldy, beta, s) : hipSuccess;
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmm beta");
+    }
+    if (algo == SM_ALGO_MFMA) {   // the matrix-core SpMM (spmm_mfma.hip)
+        if (n_rhs != 32 || ldx % 2 || ldy % 2 || ((uintptr_t)X % 8) || ((uintptr_t)Y % 8) ||
+            (uint64_t)m->n_cols * (uint64_t)ldx * 4u >= 0xFFFFFFF0ull)
+            return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_MFMA needs n_rhs = 32, even ldx/ldy, 8-byte "
+                        "aligned X/Y and X under 4 GiB");
+        e = launch_spmm_mfma(n, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X, ldx, m->n_cols,
+                             Y, ldy, alpha, beta, s);
+        e = after_launch(e, s, "sm_spmm mfma");
+        return e == hipSuccess ? SM_OK : hip_fail(e, "sm_spmm mfma");
     }
     const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
                         ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;

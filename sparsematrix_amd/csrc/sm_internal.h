@@ -219,6 +219,10 @@ hipError_t launch_spmv_ccsell(const CcsellDev &cd, const float *x, float *y, flo
 hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *a, int32_t lda,
                                    float *c, int32_t ldc, float alpha, float beta, hipStream_t s);
 // Balanced-band kind (kernels_band2.hip).
+// Gathered chunk bands (gcb.h, kernels_gcb.hip): d_chunk_start = tile -> first band,
+// d_band_clo, d_word = the lane-interleaved entries (kGcbBandWords per band).
+hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x, float *y,
+                           float alpha, float beta, hipStream_t s);
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
 // xp[rank[c]] = x[c], c < n (rank: original column -> new column).
@@ -233,6 +237,9 @@ hipError_t launch_spmm_generic(int32_t n, int32_t nrhs, const int32_t *rp, const
                                float *Y, int64_t y_sj, int64_t y_si, float alpha, float beta,
                                bool rhs_fastest, hipStream_t s);
 // Row-major X (k x nrhs, ldx) / Y (n x nrhs, ldy), nrhs % 4 == 0, 16-byte aligned.
+hipError_t launch_spmm_mfma(int32_t n, const int32_t *rp, const int32_t *col, const float *val,
+                            int32_t nnz, const float *X, int64_t ldx, int64_t x_rows, float *Y,
+                            int64_t ldy, float alpha, float beta, hipStream_t s);
 hipError_t launch_spmm_rowpanel(int32_t n, int32_t nrhs, const int32_t *rp, const int32_t *col,
                                 const float *val, int32_t nnz, const float *X, int64_t ldx,
                                 int64_t x_rows, float *Y, int64_t ldy, float alpha, float beta,

@@ -28,7 +28,7 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
 //             column order so the x gathers of one wave-instruction hit a few cache
 //             lines; LDS holds only the accumulators (measured slower, kept for A/B).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5 };
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5, kXbGcb = 6 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;

@@ -129,3 +129,38 @@ def test_config5_columns_auto_ccsell_vs_oracle(sm):
     else:
         _, absum = oracle.csr_spmv_f64(rph.astype(np.int64), cih, vah, to_host(x), to_host(y0), 1.0, 0.5)
         assert_terms_close(to_host(ya), want, absum)
+
+
+def test_config5_rank0_slice_full_size_auto_vs_oracle(sm):
+    """the slice bench.py times for config 5 (`--workload config5
+    --emulate-world 8`, and rank 0 of the 8-GPU run): rank 0's FULL 2^23 rows x 2^26 global
+    columns, 16 distinct uniform columns per row, seed 5 (bench.py: seed0 + 1000 k +
+    7919 rank), AUTO.  AUTO must build the gather-band kind (has_xband == 3) the bench
+    measures; its SpMV is compared with the oracle's same-order CSR SpMV over all 2^23
+    rows: bit for bit with one slab (rows summed in the reference's order), within
+    1e-6 * sum|terms| with several (slab sums in slab order)."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n_rows, n_cols = 1 << 23, 1 << 26
+    rp, ci, va = synth.uniform_rows_device(n_rows, n_cols, 16, seed=5)
+    A = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    info = A.info()
+    assert info["has_xband"] == 3, info          # the gather-band kind, as bench.py reports
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.rand(n_cols, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n_rows, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    A.spmv(x, y, 1.0, 0.5)
+    y2 = y0.clone()
+    A.spmv(x, y2, 1.0, 0.5)                      # deterministic: a second launch, same bits
+    got, got2 = to_host(y), to_host(y2)
+    assert np.array_equal(bits(got), bits(got2))
+    rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+    del rp, ci, va
+    xh, y0h = to_host(x), to_host(y0)
+    want = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.0, 0.5, threads=16)
+    if info["xband_slabs"] == 1:
+        assert np.array_equal(bits(got), bits(want))
+    else:
+        _, absum = oracle.csr_spmv_f64(rph.astype(np.int64), cih, vah, xh, y0h, 1.0, 0.5)
+        assert_terms_close(got, want, absum)

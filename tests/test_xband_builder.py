@@ -106,3 +106,20 @@ def test_sweep_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sweep_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_gcb_builder_under_asan(tmp_path):
+    """Gathered-chunk-band builder (gcb.cpp), decoded as the kernel decodes it: every term
+    once, rows in ascending column order, segments on consecutive lanes of one chunk, one
+    chunk per row per band, windows and slabs respected, padding as dummies."""
+    exe = tmp_path / "gcb_asan"
+    src = [os.path.join(ROOT, "tests", "native", "gcb_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "gcb.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gcb_asan: ok" in r.stdout
