@@ -187,6 +187,8 @@ def main():
     ap.add_argument("--algo", default="auto")
     ap.add_argument("--layout", default="auto",
                     help="A/B: force the matrix layout (sm_build_opts.layout name, e.g. gcb, gather)")
+    ap.add_argument("--band-tall", type=int, default=0,
+                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2) for the config-2 matrices")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")
@@ -262,8 +264,10 @@ def main():
     for k in range(replicas):
         seed = seed0 + 1000 * k + 7919 * rank
         rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
-        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index,
-                                      opts=None if args.layout == "auto" else dict(layout=args.layout))
+        bopts = {} if args.layout == "auto" else dict(layout=args.layout)
+        if args.band_tall:
+            bopts["band_tall"] = args.band_tall
+        M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index, opts=bopts or None)
         g = torch.Generator(device=dev).manual_seed(seed + 1)
         x_local = torch.rand(C // world if world > 1 else R, generator=g, device=dev) * 2 - 1
         x_full = (None if world > 1 else
@@ -490,8 +494,25 @@ def main():
                 "mfma_source": (f"profiles/mfma_{swl}_rowpanel2.json (rocprofv3 "
                                 "SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, SQ_INSTS_VALU_MFMA_F32)"
                                 if mf else None),
-                "kernel": "spmm_rowpanel2_kernel<8> (fp32 VALU; MFMA not used: ~2 flop/B, "
-                          "DESIGN.md §3.5)"}
+                "kernel": "spmm_rowpanel2_kernel<8> (fp32 VALU, bit-exact; DESIGN.md §3.5)"}
+        if N == 32:   # the matrix-core variant (SM_ALGO_MFMA), same matrix and panel
+            try:
+                for _ in range(3):
+                    r0["M"].spmm(X, Y, 1.0, 0.5, algo="mfma")
+                torch.cuda.synchronize()
+                mm_list = event_times(torch, lambda i: r0["M"].spmm(X, Y, 1.0, 0.5, algo="mfma"), 20)
+                mm = float(np.median(mm_list))
+                mfm = load_json(f"mfma_{swl}_mfma.json")
+                spmm["mfma_variant"] = {
+                    "ms": round(mm, 4), "ms_stats": stats(mm_list),
+                    "gflops": round(2.0 * nnz * N / (mm * 1e-3) / 1e9, 1),
+                    "hbm_frac": round(sb / (mm * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "mfma_util": mfm.get("mfma_util") if mfm else None,
+                    "mfma_insts": mfm.get("mfma_insts") if mfm else None,
+                    "kernel": "spmm_mfma_kernel<8> (v_mfma_f32_16x16x4_f32 on 16-row tiles; within "
+                              "the sum|terms| bound, not bit-exact; DESIGN.md §3.5)"}
+            except Exception as exc:  # noqa: BLE001
+                spmm["mfma_variant"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
         del X, Y
 
     # ---- R-MAT (config 4) on rank 0 at N = 1 ----------------------------------------

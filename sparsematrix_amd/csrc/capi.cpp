@@ -324,7 +324,8 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                              const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
                              int32_t geo_opt, int32_t slabs, bool forced) {
     const bool tall = geo_opt == 1;
-    const B2Geom geom = !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
+    const bool half2 = geo_opt == 2 && kind == kXbCband;
+    const B2Geom geom = half2 ? kB2Half2Cb : !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
@@ -340,6 +341,10 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     const bool wide3 = false;
 #endif
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
+    if (geo_opt == 2) {   // half2: codebook words only; otherwise the wide geometry
+        if (!cb) return SM_OK;
+        g = kB2Half2Cb;
+    }
     // Bands are fixed slots of g.chunks() * 64 entries: where a slab's density leaves
     // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
     // bytes than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).

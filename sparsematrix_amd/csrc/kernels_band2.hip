@@ -68,6 +68,11 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_B2_EAHEAD
 #define SM_B2_EAHEAD 2
 #endif
+// Slab hand-off protocol: 1 = the epoch form (xband_dev.h slab_handoff_epoch: no reset
+// round trip at the end, the commit snapshot read behind the band loop), 0 = slab_handoff.
+#ifndef SM_B2_EPOCH
+#define SM_B2_EPOCH 1
+#endif
 #ifndef SM_CB_TAB_COPIES
 #define SM_CB_TAB_COPIES 32
 #endif
@@ -112,8 +117,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
     constexpr bool TALL = GEO == 1;
-    static_assert(GEO != 2 || CB, "wide3 is a cband geometry");
-    constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb : kB2Wide;
+    static_assert((GEO != 2 && GEO != 3) || CB, "wide3 and half2 are cband geometries");
+    constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
+                                                       : GEO == 3 ? kB2Half2Cb : kB2Wide;
     constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
     constexpr int W = G.window;
@@ -185,13 +191,24 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // robin), so tile = the i / 8-th of XCD (i % 8)'s contiguous range of tiles: the
     // slabs of one row block share an XCD and their hand-off stays in its L2.
     int32_t t = blockIdx.x;
-    if (xcd_map) {
+    if (xcd_map == 1) {
         const int32_t G = gridDim.x, xc = t & 7, k = t >> 3;
         t = xc * (G >> 3) + min(xc, G & 7) + k;
+    } else if (xcd_map == 2 && n_slabs == 4 && gridDim.x == 256) {
+        // XCD pairs (development A/B): XCDs 2j and 2j+1 hold the blocks b = j (mod 4), slabs
+        // 0-1 on the first and 2-3 on the second -- two slabs of x per L2, and each
+        // block's hand-off crosses the fabric between two XCDs instead of four.
+        const int32_t xc = t & 7, k = t >> 3;
+        const int32_t b2 = (xc >> 1) + 4 * (k >> 1);
+        t = 4 * b2 + 2 * (xc & 1) + (k & 1);
     }
     const int32_t b = t / n_slabs;
     const int32_t slab = t - b * n_slabs;
+#if SM_B2_EPOCH
+    const uint32_t old_started = (ABL & 8) ? 0u : handoff_begin(ctl + (int64_t)b * kCtlWords, n_slabs);
+#else
     if (!(ABL & 8)) handoff_started(ctl + (int64_t)b * kCtlWords, n_slabs);
+#endif
     const int32_t g0 = tile_band_start[t];
     const int32_t nb = tile_band_start[t + 1] - g0;
     const int32_t r0 = b * block_rows;
@@ -506,6 +523,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
     if constexpr (!kDma) store_x(0, X[0]);
     __syncthreads();
+#if SM_B2_EPOCH
+    // The commit check's snapshot (xband_dev.h slab_handoff_epoch): read now, used after the
+    // band loop, so its round trip hides behind the loop.
+    const uint32_t snap = (ABL & 8) ? 0u : handoff_snapshot(ctl + (int64_t)b * kCtlWords, n_slabs);
+#endif
 
     // Whole groups of U bands (static ring indices, no branch around a load or a
     // ring register: either makes hipcc copy registers and drain vmcnt).  Steps past
@@ -595,8 +617,13 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
     __syncthreads();   // every wave is past its last x read: the hand-off words live there
     int32_t *s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
+#if SM_B2_EPOCH
+    slab_handoff_epoch<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
+                                   nr, slab, n_slabs, y_vec, old_started, snap);
+#else
     slab_handoff<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
                              nr, slab, n_slabs, y_vec);
+#endif
     flush_prof();
 }
 
@@ -607,8 +634,9 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (xb.n_blocks <= 0) return hipSuccess;
     const bool cb = xb.kind == kXbCband;
     const bool wide3 = cb && xb.band_cols == kB2Wide3Cb.window;
-    const bool tall = !wide3 && xb.band_cols != kB2Wide.window;
-    const B2Geom g = wide3 ? kB2Wide3Cb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+    const bool half2 = cb && xb.band_cols == kB2Half2Cb.window;
+    const bool tall = !wide3 && !half2 && xb.band_cols != kB2Wide.window;
+    const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -636,6 +664,15 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         const char *e = dev_env("SM_BAND2_PRIO");
         return e ? atoi(e) : 2;
     }();
+    if (half2) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true, 3); break;
+        case 8: SM_B2(8, 2, true, 3); break;
+        case 2048: SM_B2(2048, 2, true, 3); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (wide3) {
         switch (abl) {
         case 0: SM_B2(0, 2, true, 2); break;
@@ -740,7 +777,9 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     }
 #else
     if (wide3) return hipErrorInvalidValue;   // development builds only
-    if (tall) {
+    if (half2) {
+        SM_B2(0, 2, true, 3);
+    } else if (tall) {
         if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {
         if (cb) SM_B2(0, 2, true, 0); else SM_B2(0, 2, false, 0);

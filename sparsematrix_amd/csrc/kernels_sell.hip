@@ -14,7 +14,10 @@
 #include "sm_internal.h"
 #include "sell.h"
 
+#include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace smamd {
 namespace {
@@ -67,7 +70,13 @@ __global__ __launch_bounds__(kSellThreads) void spmv_sell_kernel(
 // alpha) in LDS (kTabCopies copies, lane l reads copy l % kTabCopies: fewer bank
 // conflicts), so each term is x * fl(v * alpha) -- the same bits as the plain form.
 constexpr int kCsellTabCopies = 4;
-template <int U>
+#ifdef SM_DEV
+// TS (development builds, SM_SELL_TS=1): lane 0 of every slice's wave stores the wall clock
+// (s_memrealtime, 100 MHz) at its start and end here (slices < kSellTsMax).
+constexpr int64_t kSellTsMax = 1 << 18;
+__device__ unsigned long long g_sell_ts[2 * kSellTsMax];
+#endif
+template <int U, bool TS = false, int ABL = 0, bool PIPE = true>
 __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
@@ -85,6 +94,11 @@ __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * (kSellThreads / 64) + (threadIdx.x >> 6);
     if (s >= n_slices) return;   // wave-uniform, after the only barrier
+#ifdef SM_DEV
+    if constexpr (TS) {
+        if (lane == 0 && s < kSellTsMax) g_sell_ts[2 * s] = wall_clock64();
+    }
+#endif
     const int64_t base = off[s];
     const int32_t L = len[s];
     const int32_t r = row[s * kSellLanes + lane];
@@ -94,14 +108,57 @@ __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     const uint32_t *w = word + base + lane;
     const int cp = lane & (kCsellTabCopies - 1);
     constexpr uint32_t kColMask = (1u << kSellCbColBits) - 1u;
-    for (int32_t j = 0; j < L; j += U) {
+    int32_t j = 0;
+    if (PIPE && L >= 4 * U) {
+        // Long slices (a lane walks up to 2048 slots): a chain of dependent memory round
+        // trips per group of U slots -- word load, then x gather -- made a few long waves
+        // the kernel's tail.  Software-pipelined: the words of group g+3 and the x values
+        // of group g+1 are in flight while group g is added (rings with static roles, four
+        // groups per iteration; loads past the slice read the next slice's slots or the
+        // layout's zero tail and are never added).
+        uint32_t W[4][U];
+        float XG[2][U], TV[2][U];
+        auto ld_w = [&](int32_t jj, uint32_t *dst) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) dst[u] = __builtin_nontemporal_load(w + (int64_t)(jj + u) * kSellLanes);
+        };
+        auto ld_x = [&](const uint32_t *src, float *xg, float *tv) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                xg[u] = x[(ABL & 1) ? 0u : (src[u] & kColMask)];
+                tv[u] = tab[(src[u] >> kSellCbColBits) * kCsellTabCopies + cp];
+            }
+        };
+        auto add = [&](int32_t jj, const float *xg, const float *tv) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float t = __fmul_rn(xg[u], tv[u]);
+                if (jj + u < n) acc = __fadd_rn(acc, t);
+            }
+        };
+        ld_w(0, W[0]);
+        ld_w(U, W[1]);
+        ld_w(2 * U, W[2]);
+        ld_x(W[0], XG[0], TV[0]);
+        const int32_t L4 = L & ~(4 * U - 1);   // whole iterations of four groups
+        for (; j < L4; j += 4 * U) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t jj = j + k * U;
+                ld_w(jj + 3 * U, W[(k + 3) & 3]);
+                ld_x(W[(k + 1) & 3], XG[(k + 1) & 1], TV[(k + 1) & 1]);
+                add(jj, XG[k & 1], TV[k & 1]);
+            }
+        }
+    }
+    for (; j < L; j += U) {
         uint32_t ww[U];
         float xg[U], tv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) ww[u] = __builtin_nontemporal_load(w + (int64_t)(j + u) * kSellLanes);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            xg[u] = x[ww[u] & kColMask];
+            xg[u] = x[(ABL & 1) ? 0u : (ww[u] & kColMask)];
             tv[u] = tab[(ww[u] >> kSellCbColBits) * kCsellTabCopies + cp];
         }
 #pragma unroll
@@ -112,7 +169,57 @@ __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     }
     if (r >= 0) y[r] = acc;
     else if (r < -1) partials[-2 - r] = acc;
+#ifdef SM_DEV
+    if constexpr (TS) {
+        if (lane == 0 && s < kSellTsMax) g_sell_ts[2 * s + 1] = wall_clock64();
+    }
+#endif
 }
+
+#ifdef SM_DEV
+// Timeline of the last TS launch (SM_SELL_TS): per slice length class, how many slices,
+// their mean duration and latest end; when 50 / 90 / 99 / 100 % of the slices had ended;
+// and the kernel's span -- where the time of the slice kernel goes.
+void sell_ts_report(const SellDev &sd, hipStream_t s) {
+    const int64_t ns = std::min<int64_t>(sd.n_slices, kSellTsMax);
+    std::vector<unsigned long long> h((size_t)(2 * ns));
+    std::vector<int32_t> len((size_t)ns);
+    void *sym = nullptr;
+    if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_sell_ts)) != hipSuccess) return;
+    (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(len.data(), sd.d_len, (size_t)ns * 4, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int64_t i = 0; i < ns; i++) {
+        t0 = std::min(t0, h[(size_t)(2 * i)]);
+        t1 = std::max(t1, h[(size_t)(2 * i + 1)]);
+    }
+    std::vector<double> ends((size_t)ns);
+    struct Cls { int64_t n = 0; double dur = 0, last = 0, first = 1e30, slots = 0; };
+    Cls cls[13];
+    for (int64_t i = 0; i < ns; i++) {
+        const double a = (h[(size_t)(2 * i)] - t0) * 0.01, b = (h[(size_t)(2 * i + 1)] - t0) * 0.01;
+        ends[(size_t)i] = b;
+        int k = 0;
+        while (k < 12 && (1 << (k + 1)) <= len[(size_t)i]) k++;
+        cls[k].n++;
+        cls[k].dur += b - a;
+        cls[k].last = std::max(cls[k].last, b);
+        cls[k].first = std::min(cls[k].first, a);
+        cls[k].slots += len[(size_t)i];
+    }
+    std::vector<double> se = ends;
+    std::sort(se.begin(), se.end());
+    fprintf(stderr, "sell timeline: %lld slices, span %.1f us; 50/90/99/100 %% of the slices ended by "
+            "%.1f / %.1f / %.1f / %.1f us\n", (long long)ns, (t1 - t0) * 0.01, se[(size_t)(ns / 2)],
+            se[(size_t)(9 * ns / 10)], se[(size_t)(99 * ns / 100)], se.back());
+    for (int k = 0; k < 13; k++)
+        if (cls[k].n)
+            fprintf(stderr, "  len [%5d, %5d): %7lld slices, %9.0f slot rows, mean %7.2f us, first start %7.1f, "
+                    "last end %7.1f us\n", 1 << k, 2 << k, (long long)cls[k].n, cls[k].slots,
+                    cls[k].dur / cls[k].n, cls[k].first, cls[k].last);
+}
+#endif
 
 }  // namespace
 
@@ -147,8 +254,30 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         const char *e = dev_env("SM_SELL_UNROLL");
         return e ? atoi(e) : 8;
     }();
-    if (sd.d_table) {
+    static const bool ts = dev_env("SM_SELL_TS") != nullptr;
+    if (sd.d_table && abl == 1) {   // the gathers ablated (one broadcast address), with the timeline
+        hipLaunchKernelGGL((spmv_csell_kernel<8, true, 1>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
+                           sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
+                           reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size, x, y,
+                           sd.d_partials, alpha, beta);
+        if (ts) sell_ts_report(sd, s);
+    } else if (sd.d_table && ts) {
+        hipLaunchKernelGGL((spmv_csell_kernel<8, true>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
+                           sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
+                           reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size, x, y,
+                           sd.d_partials, alpha, beta);
+        sell_ts_report(sd, s);
+    } else if (sd.d_table) {
+        static const bool nopipe = [] {
+            const char *e = dev_env("SM_SELL_PIPE");
+            return e && atoi(e) == 0;
+        }();
         if (unroll == 16) SM_CSELL_K(16);
+        else if (nopipe)   // the round-3 loop (A/B)
+            hipLaunchKernelGGL((spmv_csell_kernel<8, false, 0, false>), dim3((unsigned)grid), dim3(kSellThreads),
+                               0, s, sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
+                               reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size, x, y,
+                               sd.d_partials, alpha, beta);
         else SM_CSELL_K(8);
     } else if (abl == 1) SM_SELL_K(8, 1);
     else if (unroll == 16) SM_SELL_K(16, 0);

@@ -36,6 +36,7 @@ constexpr int kNatThreads = 256;
 constexpr int kNatPer = 16;                          // entries per thread per batch
 constexpr int kNatBatch = kNatThreads * kNatPer;     // 4096
 constexpr int kNatCols = 64;                         // output columns per workgroup
+constexpr int kNs1MaxBatches = 16;                   // native_spmv_kernel: panels up to this long
 constexpr int kNatWords = 128;                       // bitmap words per column (4096 rows)
 constexpr int kNatStride = kNatWords + 4;            // word w of column c at c*132 + w + w/32:
                                                      // the 4 quarter readers of one column,
@@ -499,6 +500,204 @@ __global__ __launch_bounds__(X1 ? 64 : kNatThreads) void native_apply_kernel(
     }
 }
 
+// ---- m = 1: one workgroup per panel, a stable counting sort per batch ----------------
+// Thread t owns output column t of the panel (its running sum lives in a register for the
+// whole panel).  Per batch of 4096 entries (16 contiguous entries per thread):
+//   decode   the thread's delta sum, a wave scan, the wave totals (LDS) and the carry give
+//            every entry its in-panel offset (kernel.cc:780-782); live entries (id < T) load
+//            x[row] -- the NEXT batch is decoded and its x gathers issued while this batch is
+//            sorted and applied, so their latency hides behind it;
+//   rank     each wave takes its 1024 entries in stream order, 64 at a time: eight ballots
+//            of the column bits give every lane the lanes holding the same column, so its
+//            rank among them and the group's count; a per-wave running count per column
+//            (LDS, the wave's own row of it) adds the earlier steps -- a stable rank by
+//            column without atomics;
+//   offsets  thread t sums column t's four wave counts, a block scan over the columns gives
+//            each (wave, column) its list start;
+//   scatter  every live entry stores its term fl(x * fl(table[id] * alpha)) (kernel.cc:791)
+//            at list start + rank: per column, the batch's terms in stream (= row) order;
+//   apply    thread t adds column t's terms in that order (separate roundings).
+// So each output receives its terms exactly in the reference's order after beta.  About
+// 2-3 K cycles of LDS and ballot work per batch, against the bitmap kernel's 14-17 K.
+constexpr int kNs1Waves = kNatThreads / 64;
+
+__device__ __forceinline__ int32_t block_excl_scan256(int32_t v, int32_t *wtot) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int32_t incl = wave_incl_scan(v, lane);
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int32_t base = 0;
+#pragma unroll
+    for (int w = 0; w < kNs1Waves; ++w)
+        if (w < wave) base += wtot[w];
+    return base + incl - v;
+}
+
+__global__ __launch_bounds__(kNatThreads) void native_spmv_kernel(
+    const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
+    const int64_t *__restrict__ pbeg, const int64_t *__restrict__ pend,
+    const int32_t *__restrict__ pcol, const float *__restrict__ table, int32_t T, int32_t n,
+    const float *__restrict__ x, float *__restrict__ y, float alpha, float beta) {
+    __shared__ float tab[256];
+    __shared__ uint16_t lc[kNatBatch];                 // column of entry e (0x100: dead)
+    __shared__ float lt[kNatBatch];                    // its term
+    __shared__ float ls[kNatBatch + 1];                // terms by column (+ the dead entries' slot)
+    __shared__ int32_t wcnt[kNs1Waves][256];           // running counts, then list starts
+    __shared__ int32_t wsum[2][kNs1Waves];
+    __shared__ int32_t wtot[kNs1Waves];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int32_t p = blockIdx.x;
+    const int32_t col = pcol[p] + t;
+    const bool own = col < n;
+    tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
+#pragma unroll
+    for (int w = 0; w < kNs1Waves; ++w) wcnt[w][t] = 0;
+    float acc = 0.0f;
+    if (own) {
+        acc = y[col];
+        if (beta != 1.0f) acc = __fmul_rn(acc, beta);
+    }
+    const int64_t e_beg = pbeg[p], e_end = pend[p];
+    auto load = [&](int64_t e0, uint4 &dv, uint4 &iv) {
+        const int64_t e = e0 + (int64_t)t * kNatPer;
+        if (e + kNatPer <= e_end) {   // panel runs start 16-byte aligned (upload_native)
+            dv = *reinterpret_cast<const uint4 *>(pos + e);
+            iv = *reinterpret_cast<const uint4 *>(val + e);
+        } else {
+            uint8_t d[kNatPer], id[kNatPer];
+#pragma unroll
+            for (int k = 0; k < kNatPer; ++k) {
+                const bool in = e + k < e_end;
+                d[k] = in ? pos[e + k] : 0;
+                id[k] = in ? val[e + k] : 255;   // >= T: dead
+            }
+            __builtin_memcpy(&dv, d, 16);
+            __builtin_memcpy(&iv, id, 16);
+        }
+    };
+    // Decode, part 1 (before a barrier): the thread's delta sum and its wave's inclusive scan.
+    // Part 2 (after it): offsets, live flags and the x gathers of live entries.
+    int32_t carry = 0;
+    uint4 dv_c = {0, 0, 0, 0}, iv_c = {0, 0, 0, 0}, dv_n = {0, 0, 0, 0}, iv_n = {0, 0, 0, 0};
+    int32_t cpos[kNatPer];      // current batch: offset (dead: -1)
+    float cx[kNatPer];          // current batch: x of live entries
+    uint8_t cid[kNatPer];
+    auto decode1 = [&](const uint4 &dv, int buf) -> int32_t {   // returns the thread's exclusive prefix
+        uint8_t d[kNatPer];
+        __builtin_memcpy(d, &dv, 16);
+        int32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < kNatPer; ++k) tot += d[k];
+        const int32_t incl = wave_incl_scan(tot, lane);
+        if (lane == 63) wsum[buf][wave] = incl;
+        return incl - tot;
+    };
+    auto decode2 = [&](const uint4 &dv, const uint4 &iv, int buf, int32_t excl) {
+        uint8_t d[kNatPer];
+        __builtin_memcpy(d, &dv, 16);
+        __builtin_memcpy(cid, &iv, 16);
+        int32_t off = carry + excl, batch_total = 0;
+#pragma unroll
+        for (int w = 0; w < kNs1Waves; ++w) {
+            if (w < wave) off += wsum[buf][w];
+            batch_total += wsum[buf][w];
+        }
+        carry += batch_total;
+#pragma unroll
+        for (int k = 0; k < kNatPer; ++k) {
+            off += d[k];
+            const bool live = cid[k] < T;
+            cpos[k] = live ? off : -1;
+            cx[k] = live ? x[off >> 8] : 0.0f;   // gathers in flight through the sort below
+        }
+    };
+    int64_t e0 = e_beg;
+    if (e0 < e_end) load(e0, dv_c, iv_c);
+    int32_t ex = decode1(dv_c, 0);
+    __syncthreads();   // tab, wcnt, wsum[0]
+    if (e0 < e_end) decode2(dv_c, iv_c, 0, ex);
+    if (e0 + kNatBatch < e_end) load(e0 + kNatBatch, dv_n, iv_n);
+    int buf = 1;
+    for (; e0 < e_end; e0 += kNatBatch, buf ^= 1) {
+        // The current batch's columns and terms into LDS, in batch (= stream) order.
+#pragma unroll
+        for (int k = 0; k < kNatPer; ++k) {
+            const bool live = cpos[k] >= 0;
+            lc[t * kNatPer + k] = live ? (uint16_t)(cpos[k] & 255) : (uint16_t)0x100;
+            lt[t * kNatPer + k] = live ? __fmul_rn(cx[k], tab[cid[k]]) : 0.0f;
+        }
+        // The next batch's decode, part 1.
+        const bool more = e0 + kNatBatch < e_end;
+        uint4 dv_x = dv_n, iv_x = iv_n;
+        ex = decode1(dv_x, buf);
+        if (e0 + 2 * kNatBatch < e_end) load(e0 + 2 * kNatBatch, dv_n, iv_n);   // two ahead
+        __syncthreads();
+        // Rank: this wave's 1024 entries, 64 per step, in stream order.
+        int32_t rk[kNatPer], cc[kNatPer];
+        float tv[kNatPer];
+#pragma unroll
+        for (int s2 = 0; s2 < kNatPer; ++s2) {
+            const int e = 1024 * wave + 64 * s2 + lane;
+            const int32_t c = lc[e];
+            tv[s2] = lt[e];
+            const bool live = c < 256;
+            uint64_t same = __ballot(live);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint64_t mb = __ballot((c >> b) & 1);
+                same &= ((c >> b) & 1) ? mb : ~mb;
+            }
+            const uint64_t below = same & ((1ull << lane) - 1ull);
+            const int32_t cl = c & 255;
+            const int32_t base = wcnt[wave][cl];
+            rk[s2] = base + __popcll(below);
+            cc[s2] = live ? cl : -1;
+            if (live && (same >> lane) == 1ull) wcnt[wave][cl] = base + __popcll(same);
+        }
+        __syncthreads();
+        // Offsets: column t's four wave counts, a scan over the columns.
+        int32_t cn[kNs1Waves], ctot = 0;
+#pragma unroll
+        for (int w = 0; w < kNs1Waves; ++w) {
+            cn[w] = wcnt[w][t];
+            ctot += cn[w];
+        }
+        const int32_t cbase = block_excl_scan256(ctot, wtot);   // (one barrier inside)
+        {
+            int32_t b = cbase;
+#pragma unroll
+            for (int w = 0; w < kNs1Waves; ++w) {
+                wcnt[w][t] = b;
+                b += cn[w];
+            }
+        }
+        // The next batch's decode, part 2 (wsum[buf] is final): offsets and x gathers.
+        if (more) decode2(dv_x, iv_x, buf, ex);
+        __syncthreads();
+        // Scatter (dead entries write the spare slot).
+#pragma unroll
+        for (int s2 = 0; s2 < kNatPer; ++s2) {
+            const int32_t slot = cc[s2] >= 0 ? wcnt[wave][cc[s2]] + rk[s2] : kNatBatch;
+            ls[slot] = tv[s2];
+        }
+        __syncthreads();
+        // Apply column t's terms in order; the counts restart at zero.
+        if (own) {
+            int32_t s = cbase;
+            const int32_t s1 = cbase + ctot;
+            for (; s + 4 <= s1; s += 4) {
+                const float a0 = ls[s], a1 = ls[s + 1], a2 = ls[s + 2], a3 = ls[s + 3];
+                acc = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(acc, a0), a1), a2), a3);
+            }
+            for (; s < s1; ++s) acc = __fadd_rn(acc, ls[s]);
+        }
+#pragma unroll
+        for (int w = 0; w < kNs1Waves; ++w) wcnt[w][t] = 0;
+        __syncthreads();
+    }
+    if (own) y[col] = acc;
+}
+
 }  // namespace
 
 hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *a, int32_t lda,
@@ -508,6 +707,19 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
     if (!nd.d_pos || !nd.d_val || !nd.d_beg || !nd.d_end || !nd.d_col || !nd.d_table ||
         nd.table_size < 0 || nd.table_size > 255 || nd.s_rows >= ((int64_t)1 << 23))
         return hipErrorInvalidValue;
+    // m = 1 with panels of up to kNs1MaxBatches batches: one workgroup per panel, the
+    // counting-sort kernel above (a longer panel is one workgroup's serial chain: the
+    // two-kernel form below spreads its batches instead).
+    bool ns1 = m == 1 && nd.max_panel_batches <= kNs1MaxBatches;
+#ifdef SM_DEV
+    if (const char *e = dev_env("SM_NAT_SORT")) ns1 = m == 1 && atoi(e) != 0;   // A/B
+#endif
+    if (ns1) {
+        hipLaunchKernelGGL(native_spmv_kernel, dim3((unsigned)P), dim3(kNatThreads), 0, s, nd.d_pos, nd.d_val,
+                           nd.d_beg, nd.d_end, nd.d_col, nd.d_table, nd.table_size, (int32_t)nd.s_cols, a, c,
+                           alpha, beta);
+        return hipGetLastError();
+    }
     if (nd.max_panel_batches > kNatFusedBatches && nd.d_lists) {
         // Two kernels: decode every (batch, group) at once, then walk the lists.
         const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;

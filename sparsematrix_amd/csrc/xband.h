@@ -128,6 +128,11 @@ constexpr B2Geom kB2Wide{1 << 14, 8192, 14};
 constexpr B2Geom kB2TallB2{1 << 15, 4096, 13};
 constexpr B2Geom kB2TallCb{1 << 15, 3840, 13, 2, kCbColBits, 1};
 constexpr B2Geom kB2Wide3Cb{1 << 14, 12160, 14, 3, 14, 1};
+// half2 (cband only): 8K-row blocks (32 KiB of sums) and 15872-column windows (2 x 62 KiB),
+// the table in 4 copies -- 160 KiB of LDS exactly.  Config 2 takes 2 slabs of 512K columns
+// (128 blocks x 2 = 256 tiles): twice the x per term of the wide geometry, but each tile hands
+// off half its sums to ONE sibling instead of three quarters to three.
+constexpr B2Geom kB2Half2Cb{1 << 13, 15872, 14, 2, 14, 4};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

@@ -40,7 +40,7 @@ def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
                                  opts=dict(layout=kind, band_tall=tall, band_slabs=slabs or 0))
     info = M.info()
     assert info["has_xband"] == KINDS[kind], info
-    assert info["xband_block_rows"] <= (32768 if tall else 16384), info
+    assert info["xband_block_rows"] <= (32768 if tall == 1 else 8192 if tall == 2 else 16384), info
     return M, info
 
 
@@ -174,6 +174,41 @@ def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
         assert np.array_equal(bits(to_host(y)), first)
     want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"])
     assert np.array_equal(first, bits(want))
+
+
+@pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
+def test_cband_half2_vs_oracle(sm, n_rows, n_cols, per_row):
+    """The half2 geometry (8K-row blocks, 15872-column windows, 4 table copies):
+    bit-identical to the slab-order oracle (one slab: the reference's order)."""
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + 3 * n_cols)
+    for slabs in (1, None):
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, "cband", 2)
+        assert info["xband_block_rows"] <= 8192, info
+        rng = np.random.default_rng(8)
+        x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+        y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+        for alpha, beta in ((1.0, 0.5), (1.3, 0.0)):
+            _check(M, info, rp, ci, va, x, y0, alpha, beta)
+
+
+def test_cband_half2_config2_vs_slab_oracle(sm):
+    """Config 2 (2^20 x 2^20, 16 per row) in the half2 geometry: 2 slabs of 524288 columns,
+    bit-identical to the 2-slab restatement of the reference order."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=2))
+    info = M.info()
+    assert info["has_xband"] == 5 and info["xband_slabs"] == 2 and info["xband_block_rows"] == 8192, info
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.0, 0.5)
+    want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
+                           1.0, 0.5, info["xband_slab_cols"])
+    assert np.array_equal(bits(to_host(y)), bits(want))
 
 
 def test_band2_config2_equals_blocked(sm):

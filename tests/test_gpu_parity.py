@@ -936,7 +936,8 @@ def test_native_two_streams(sm):
 
 
 @pytest.mark.parametrize("n,dens,m", [(16384, 0.001, 1), (4096, 0.25, 1), (2000, 0.05, 13),
-                                      (3000, 0.6, 32)])
+                                      (3000, 0.6, 32), (8192, 0.02, 1), (20000, 0.0002, 1),
+                                      (1000, 0.3, 1), (300, 0.9, 1)])
 def test_native_vs_oracle_larger(sm, n, dens, m):
     """Larger reference streams (fillers at 0.1 % density, dense panels at 25-60 %, long
     panels spanning many 4096-entry chunks): the native kernel equals the restated

@@ -21,6 +21,8 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--ab-env", default="SM_SPMM_OLD",
                     help="variable toggled 1 (\"old\") / 0 (\"new\"), e.g. SM_SPMM_NT")
+    ap.add_argument("--algos", default="",
+                    help="compare sm_spmm algorithms instead, e.g. auto,mfma (old = the first)")
     args = ap.parse_args()
 
     import numpy as np
@@ -41,25 +43,30 @@ def main() -> None:
         X = torch.rand((R, N), generator=g, device=dev) * 2 - 1
         Y0 = torch.rand((R, N), generator=g, device=dev) * 2 - 1
         res = {}
+        algos = args.algos.split(",") if args.algos else None
         for old in ("1", "0"):
-            os.environ[args.ab_env] = old
+            algo = "auto"
+            if algos:
+                algo = algos[0] if old == "1" else algos[1]
+            else:
+                os.environ[args.ab_env] = old
             Y = Y0.clone()
             for _ in range(3):
-                M.spmm(X, Y, 1.0, 0.5)
+                M.spmm(X, Y, 1.0, 0.5, algo=algo)
             torch.cuda.synchronize()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.reps)]
             for a, b in ev:
                 a.record()
-                M.spmm(X, Y, 1.0, 0.5)
+                M.spmm(X, Y, 1.0, 0.5, algo=algo)
                 b.record()
             torch.cuda.synchronize()
             ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
             Y = Y0.clone()
-            M.spmm(X, Y, 1.0, 0.5)
+            M.spmm(X, Y, 1.0, 0.5, algo=algo)
             res[old] = (ms, Y.cpu().numpy().view(np.uint32))
         same = bool(np.array_equal(res["0"][1], res["1"][1]))
-        line = {"ab_env": args.ab_env, "n_rhs": N, "old_ms": round(res["1"][0], 4), "new_ms": round(res["0"][0], 4),
+        line = {"ab_env": args.algos or args.ab_env, "n_rhs": N, "old_ms": round(res["1"][0], 4), "new_ms": round(res["0"][0], 4),
                 "gflops_new": round(2.0 * nnz * N / (res["0"][0] * 1e-3) / 1e9, 1),
                 "bit_identical": same}
         print(json.dumps(line), flush=True)
