@@ -256,6 +256,10 @@ bool kind_forced(const sm_matrix *m) {
 // 77 / 73, 8M 145 vs - / 93 us.  Past ~3M columns each blocked tile sweeps more x
 // through LDS than gathering its terms' x costs.
 constexpr int64_t kGatherCols = 3 * ((int64_t)1 << 20);   // gather kind: > 3M columns
+// Gathered chunk bands (gcb.h): past 16M columns (config 5's 64M-column rank slices: 0.83 vs
+// 1.61 ms for the gather kind) -- the gather kind's 32K-column bands hold too
+// few terms there; where the gather kind's own cost model accepts a band layout.
+constexpr int64_t kGcbCols = (int64_t)1 << 24;
 
 XbKind xband_kind_setting(const sm_matrix *m) {
     switch (m->opts.layout) {
@@ -267,7 +271,7 @@ XbKind xband_kind_setting(const sm_matrix *m) {
     case SM_LAYOUT_GCB: return kXbGcb;
     default: break;
     }
-    return m->n_cols > kGatherCols ? kXbGather : kXbCband;
+    return m->n_cols >= kGcbCols ? kXbGcb : m->n_cols > kGatherCols ? kXbGather : kXbCband;
 }
 
 // Sweeping x through LDS (or walking its bands) pays when the L2 -> LDS bytes of
@@ -291,8 +295,8 @@ static bool gather_cost_ok(const sm_matrix *m) {
 }
 
 static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
-    if (kind == kXbGather && m->n_cols > kGatherCols && m->opts.gather_band_log2 == 0)
-        return gather_cost_ok(m);
+    if ((kind == kXbGather || kind == kXbGcb) && m->n_cols > kGatherCols && m->opts.gather_band_log2 == 0)
+        return gather_cost_ok(m);   // gcb: ~2x faster than the gather kind it is priced as
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
                           : kind == kXbBand2 || kind == kXbCband ? kB2RowBits
                           : kind == kXbGather ? kXbGatherRowsLog2

@@ -29,7 +29,9 @@ namespace {
 
 constexpr int kGcbThreads = 1024;
 
-template <int ROWS_LOG2, int ER, int GA>
+// ABL (development builds, SM_GCB_ABLATE; results wrong): 1 no x gathers (x read as 0,
+// no memory request), 2 no apply (the loaded values kept live), 4 no per-band barrier.
+template <int ROWS_LOG2, int ER, int GA, int ABL = 0>
 __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
@@ -84,7 +86,8 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint32_t w = e[k];
-            const uint32_t off = (w & kGcbLive) ? 4u * (uint32_t)(c + (int32_t)(w & kGcbColMask)) : 0xFFFFFFF0u;
+            const uint32_t off = ((w & kGcbLive) && !(ABL & 1)) ? 4u * (uint32_t)(c + (int32_t)(w & kGcbColMask))
+                                                                : 0xFFFFFFF0u;
             xv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x_src, off, 0, 0));
         }
     };
@@ -182,9 +185,14 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
             const int32_t q = p + u;
             if (q + ER >= cw + 64) advance();
             gather(q + GA, E[(u + GA) % ER], XV[(u + GA) % XR]);
-            apply(E[u % ER], XV[u % XR]);
+            if constexpr (ABL & 2) {
+                asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y), "v"(E[u % ER].z), "v"(E[u % ER].w),
+                             "v"(XV[u % XR][0]), "v"(XV[u % XR][1]));
+            } else {
+                apply(E[u % ER], XV[u % XR]);
+            }
             E[u % ER] = load_e(q + ER);
-            if (q < nb) __syncthreads();
+            if (!(ABL & 4) && q < nb) __syncthreads();
         }
     }
 
@@ -217,10 +225,30 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
                        xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
                        xb.d_tickets, alpha, beta)
     int look = 0;
+    const bool tall = xb.block_rows > (1 << 14);
 #ifdef SM_DEV
     if (const char *e = dev_env("SM_GCB_LOOK")) look = atoi(e);   // development A/B of ER/GA
+    if (const char *e = dev_env("SM_GCB_ABLATE")) {
+        const int abl = atoi(e);
+#define SM_GCBA(A)                                                                                    \
+    if (tall) hipLaunchKernelGGL((spmv_gcb_kernel<15, 6, 2, A>), grid, block, 0, s, n_rows, n_cols, xb.block_rows, \
+                                 xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
+                                 xb.d_tickets, alpha, beta);                                         \
+    else hipLaunchKernelGGL((spmv_gcb_kernel<14, 6, 2, A>), grid, block, 0, s, n_rows, n_cols, xb.block_rows, \
+                            xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
+                            xb.d_tickets, alpha, beta)
+        switch (abl) {
+        case 1: SM_GCBA(1); break;
+        case 2: SM_GCBA(2); break;
+        case 3: SM_GCBA(3); break;
+        case 4: SM_GCBA(4); break;
+        case 5: SM_GCBA(5); break;
+        default: return hipErrorInvalidValue;
+        }
+#undef SM_GCBA
+        return hipGetLastError();
+    }
 #endif
-    const bool tall = xb.block_rows > (1 << 14);
     switch (look) {
     case 42: if (tall) SM_GCB(15, 4, 2); else SM_GCB(14, 4, 2); break;
     case 63: if (tall) SM_GCB(15, 6, 3); else SM_GCB(14, 6, 3); break;

@@ -77,6 +77,7 @@ IFS=',' read -ra ST <<< "$STEPS"
 for s in "${ST[@]}"; do
   case $s in
     ab) step ab bash tools/r4_ab.sh ;;
+    ab2) step ab2 env CASES="$CASES2" ENVS="${ENVS2:-}" bash tools/r4_ab.sh ;;
     tests) step tests run_tests ;;
     bench) step bench run_bench ;;
     rehearse) step rehearse run_rehearse ;;
