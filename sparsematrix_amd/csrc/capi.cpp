@@ -1433,8 +1433,8 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->xband_block_rows = m->plan.xb.block_rows;
     info->xband_slab_cols =
         m->plan.xb.n_blocks == 0 ? 0
-        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
-            ? m->plan.xb.slab_bands   // band2 / cband keep slab columns there
+        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb
+            ? m->plan.xb.slab_bands   // band2 / cband / gcb keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
@@ -1661,15 +1661,6 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
             break;
         }
         [[fallthrough]];   // no sell layout -> stream kernel
-    case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
-        const float *xs = x;
-        if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns
-            e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
-            xs = m->plan.d_xperm;
-        }
-        if (e == hipSuccess) e = launch_spmv_sell(m->plan.xsell, xs, y, alpha, beta, s);
-        break;
-    }
     case SM_ALGO_STREAM:
         // Long-row partial sums (and the relabeled x) live in the matrix (allocated at
         // creation): SpMVs on one matrix must not run concurrently on different streams.
@@ -1683,6 +1674,15 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
                                m->plan.d_partials, s);
         break;
+    case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
+        const float *xs = x;
+        if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns
+            e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
+            xs = m->plan.d_xperm;
+        }
+        if (e == hipSuccess) e = launch_spmv_sell(m->plan.xsell, xs, y, alpha, beta, s);
+        break;
+    }
     default:
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     }

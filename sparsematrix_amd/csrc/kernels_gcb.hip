@@ -57,7 +57,8 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
     const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
     const __amdgpu_buffer_rsrc_t e_src =
         rsrc(ent + (int64_t)g0 * kGcbBandWords, (uint64_t)nb * kGcbBandWords * 4);
-    // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi).
+    // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi); the
+    // window moves on when the band gathered next leaves its low half.
     const int32_t *clg = band_clo + g0;
     int32_t cw = 0;
     int32_t clo_lo = lane < nb ? clg[lane] : 0;
@@ -183,7 +184,7 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
-            if (q + ER >= cw + 64) advance();
+            if (q + GA >= cw + 64) advance();   // the gather below reads clo of band q + GA
             gather(q + GA, E[(u + GA) % ER], XV[(u + GA) % XR]);
             if constexpr (ABL & 2) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y), "v"(E[u % ER].z), "v"(E[u % ER].w),

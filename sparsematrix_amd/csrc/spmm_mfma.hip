@@ -20,7 +20,9 @@
 // terms.  Against the reference's round(acc + round(x * fl(v * alpha))) that is one
 // rounding per term instead of two: within 1e-6 * sum|terms|, not bit-identical (the
 // row-panel kernels stay the bit-exact SpMM).  The zero entries multiply the other rows'
-// X values, so a non-finite X row turns the tile's other outputs into NaN: finite X only.
+// X values, so a non-finite X row turns the tile's other outputs into NaN: finite X only;
+// and they add fma(0, x, acc), which reads an accumulator of -0.0 (beta = 0 on a negative
+// y, with no term of its own yet) as +0.0 -- the one bit pattern that differs from the chain.
 // The A matrix is 1/16 dense (16 rows share a step's four terms), so the matrix cores do
 // 16x the useful flops -- at about 2 flop per byte the SpMM has flops to spare, and the
 // question this kernel answers is whether the gather stream runs any

@@ -569,7 +569,7 @@ def test_blas_test_cli():
     lines = [l for l in r.stdout.splitlines() if l.startswith("|")]
     assert lines[0].startswith("| | 4x64x128 |") and lines[0].count("|") == 1 + 9 + 1, lines[0]
     names = {l.split("|")[1].strip() for l in lines[1:]}
-    assert names == {"cpu_sgemm_baseline", "sgemm_sparse", "sgemm_sparse_device"}, names
+    assert names == {"cpu_sgemm_baseline", "sgemm_sparse", "sgemm_sparse_device", "sm_addmatmat_auto"}, names
     assert "failed" not in r.stdout
     # first matching pattern decides (blas_test.h:20-26): exclude the device variant first
     r = subprocess.run([exe, "8", "128", "256", "1", "-device;sparse"], capture_output=True,

@@ -14,6 +14,7 @@ IFS=';' read -ra EV <<< "${ENVS:-}"
 for i in "${!CS[@]}"; do
   name=${CS[$i]%%|*}; args=${CS[$i]#*|}
   extra=${EV[$i]:-}
+  extra=${extra//SM_LIB_PATH=build/SM_LIB_PATH=$ROOT/build}   # the run starts in /tmp
   rm -rf "$OUT/ab_$name"
   ( cd /tmp && env $extra timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ab_$name" -o run -- \
       python3 "$ROOT/bench.py" --no-cpu --no-spmm --no-rmat --no-config5 --no-fp32-values $args ) > "$OUT/ab_$name.log" 2>&1 || { tail -30 "$OUT/ab_$name.log"; exit 21; }

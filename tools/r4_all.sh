@@ -65,6 +65,15 @@ for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
 PY
   [[ $rc -eq 0 ]] || return $rc
 }
+run_sellpipe() {   # the sell tests on the dev library, pipelined loop off and on
+  local rc=0
+  for v in 0 1; do
+    SM_LIB_PATH=$ROOT/build/dev/libsparsematrix_amd.so SM_SELL_PIPE=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_sell.py -q --timeout 120 --timeout-method thread > "$OUT/r4_sellpipe$v.log" 2>&1
+    rc=$?
+    echo "-- SM_SELL_PIPE=$v rc=$rc"; tail -4 "$OUT/r4_sellpipe$v.log"
+    [[ $rc -eq 0 || $rc -eq 1 ]] || return $rc
+  done
+}
 run_spmm() { prof spmm 300 python3 "$ROOT/tools/spmm_ab.py" --algos auto,mfma --n 32; }
 run_native() { prof native 300 python3 "$ROOT/tools/native_bench.py"; }
 run_blas() {
@@ -84,6 +93,7 @@ for s in "${ST[@]}"; do
     c5) step c5 bash tools/r4_c5.sh ;;
     rmat) step rmat run_rmat ;;
     spmm) step spmm run_spmm ;;
+    sellpipe) step sellpipe run_sellpipe ;;
     native) step native run_native ;;
     blas) step blas run_blas ;;
   esac
