@@ -1159,7 +1159,7 @@ sm_status sm_create_from_dense_index(const uint8_t *index, int32_t rows, int32_t
 
 // CopyForm's scan on the device (encode_dev.hip): count, host prefix sum, fill, then the
 // device-CSR constructor (validation, plans, band layout).  Same CSR as the host
-// encoder, bit for bit; no reference stream is kept (like a CSR-built matrix).
+// encoder, bit for bit, and the same reference stream (refenc_dev.hip, from the ids).
 sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows, int32_t cols,
                                             int32_t stride, const float *table,
                                             int32_t table_size, sm_trans trans, int32_t device,
@@ -1191,10 +1191,11 @@ sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows
     std::vector<int32_t> cnt((size_t)n_cnt);
     int32_t *d_cnt = nullptr, *d_offs = nullptr, *d_rp = nullptr, *d_col = nullptr;
     float *d_table = nullptr, *d_val = nullptr;
+    uint8_t *d_ids = nullptr;
     int64_t scratch = 0;
     auto cleanup = [&]() {
         (void)hipFree(d_cnt); (void)hipFree(d_offs); (void)hipFree(d_rp);
-        (void)hipFree(d_col); (void)hipFree(d_val); (void)hipFree(d_table);
+        (void)hipFree(d_col); (void)hipFree(d_val); (void)hipFree(d_table); (void)hipFree(d_ids);
     };
     hipError_t e = dev_alloc(&d_cnt, n_cnt, scratch);
     if (e == hipSuccess)
@@ -1229,6 +1230,7 @@ sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows
     if (e == hipSuccess) e = dev_alloc(&d_table, (int64_t)tb.size(), scratch);
     if (e == hipSuccess) e = dev_alloc(&d_col, std::max<int64_t>(nnz, 1), scratch);
     if (e == hipSuccess) e = dev_alloc(&d_val, std::max<int64_t>(nnz, 1), scratch);
+    if (e == hipSuccess) e = dev_alloc(&d_ids, std::max<int64_t>(nnz, 1), scratch);
     if (e == hipSuccess)
         e = hipMemcpyAsync(d_offs, offs.data(), (size_t)n_cnt * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
@@ -1237,19 +1239,42 @@ sm_status sm_create_from_dense_index_device(const uint8_t *d_index, int32_t rows
         e = hipMemcpyAsync(d_table, tb.data(), tb.size() * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = launch_encode_fill(d_index, rows, cols, stride, tr, chunk_rows, n_chunks, T,
-                               tr ? d_rp : d_offs, d_table, d_col, d_val, s);
+                               tr ? d_rp : d_offs, d_table, d_col, d_val, d_ids, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);   // host vectors above go out of scope
     if (e != hipSuccess) { cleanup(); return hip_fail(e, "dense index fill"); }
     sm_build_opts o;   // the CopyForm path: SM_ALGO_EXACT keeps a reference-order kernel
     sm_build_opts_init(&o);
     o.exact_sell = 1;
     st = sm_create_from_csr_device_ex(nb, kb, nnz, d_rp, d_col, d_val, device, stream, &o, out);
-    cleanup();
     if (st == SM_OK) {
-        (*out)->from_index = true;
-        (*out)->table_size = table_size;
-        (*out)->table = std::move(tb);
+        sm_matrix *m = *out;
+        m->from_index = true;
+        m->table_size = table_size;
+        m->table = std::move(tb);
+        // The reference stream from the index's own ids (refenc_dev.hip), as the host
+        // constructor keeps it; S rows >= 2^23 (the reference's int32 offsets) keep none.
+        EncodeResult er;
+        hipError_t he = hipSuccess;
+        const int rc = encode_csr_ref_device(d_rp, d_col, d_val, d_ids, nb, kb, nnz, table, table_size, er, s, he);
+        if (rc == 0) {
+            m->has_ref = true;
+            m->pos = std::move(er.pos);
+            m->val = std::move(er.val_id);
+            m->panel_row_off = std::move(er.panel_row_off);
+            m->panel_col_off = std::move(er.panel_col_off);
+            m->panel_begin = std::move(er.panel_begin);
+            m->panel_end = std::move(er.panel_end);
+            st = upload_native(m);
+        } else if (rc != -4) {
+            st = rc == -5 ? hip_fail(he, "dense index reference stream")
+                          : fail(SM_ERR_INVALID_ARG, "dense index reference stream (%d)", rc);
+        }
+        if (st != SM_OK) {
+            sm_destroy(m);
+            *out = nullptr;
+        }
     }
+    cleanup();
     return st;
 }
 
@@ -1476,13 +1501,13 @@ sm_status sm_build_ref_stream(sm_matrix *m, const float *table, int32_t table_si
     if (table && (table_size < 0 || table_size > 255))
         return fail(SM_ERR_INVALID_ARG, "table_size %d not in [0, 255]", table_size);
     DeviceGuard g(m->device);
-    std::vector<int32_t> rp((size_t)m->n_rows + 1), col((size_t)m->nnz);
-    std::vector<float> val((size_t)m->nnz);
-    sm_status st = sm_copy_csr(m, rp.data(), col.data(), val.data());
-    if (st != SM_OK) return st;
+    // On the device (refenc_dev.hip): sort, gaps, scan and emit; the host keeps the stream's
+    // copy (sm_copy_ref_stream, sm_equal) and derives the native layout's batch metadata.
     EncodeResult er;
-    const int rc = encode_csr_ref(rp.data(), col.data(), val.data(), m->n_rows, m->n_cols, table,
-                                  table_size, er);
+    hipError_t he = hipSuccess;
+    const int rc = encode_csr_ref_device(m->d_row_ptr, m->d_col, m->d_val, nullptr, m->n_rows, m->n_cols,
+                                         m->nnz, table, table_size, er, nullptr, he);
+    if (rc == -5) return hip_fail(he, "sm_build_ref_stream");
     if (rc == -2) return fail(SM_ERR_INVALID_ARG, "a value is not in the codebook");
     if (rc == -3) return fail(SM_ERR_NOT_SUPPORTED, "more than 255 distinct values: no uint8 ids");
     if (rc == -4) return fail(SM_ERR_NOT_SUPPORTED, "S rows >= 2^23: the reference's int32 offsets overflow");
@@ -1496,7 +1521,7 @@ sm_status sm_build_ref_stream(sm_matrix *m, const float *table, int32_t table_si
     m->panel_begin = std::move(er.panel_begin);
     m->panel_end = std::move(er.panel_end);
     m->has_ref = true;
-    st = upload_native(m);
+    const sm_status st = upload_native(m);
     if (st != SM_OK) {   // no half-built encoding -- a retry starts over
         free_native_dev(m->plan.nat);
         m->has_ref = false;

@@ -5,7 +5,8 @@
 // and table[id] of every id < table_size of S column j.
 //   NoTrans (S = index):   B row j = column j of the index (strided bytes);
 //   Trans   (S = index^T): B row j = row j of the index (contiguous bytes).
-// Two passes (count, fill) around a host prefix sum of the counts: the count
+// The fill pass can also keep each term's id (ids != null) for the reference stream
+// (refenc_dev.hip).  Two passes (count, fill) around a host prefix sum of the counts: the count
 // arrays are small (one int per B row, or per (row chunk, B row)), and the
 // matrix constructor copies row_ptr to the host for its plans anyway.
 #include "sm_internal.h"
@@ -25,7 +26,8 @@ __global__ __launch_bounds__(256) void encode_cols_kernel(const uint8_t *__restr
                                                           const int32_t *__restrict__ offs,
                                                           const float *__restrict__ table,
                                                           int32_t *__restrict__ col,
-                                                          float *__restrict__ val) {
+                                                          float *__restrict__ val,
+                                                          uint8_t *__restrict__ ids) {
     const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t ch = blockIdx.y;
     if (j >= cols) return;
@@ -44,6 +46,7 @@ __global__ __launch_bounds__(256) void encode_cols_kernel(const uint8_t *__restr
         if (id < T) {
             col[o] = r;
             val[o] = table[id];
+            if (ids) ids[o] = id;
             ++o;
         }
     }
@@ -57,7 +60,8 @@ __global__ __launch_bounds__(256) void encode_rows_kernel(const uint8_t *__restr
                                                           const int32_t *__restrict__ row_ptr,
                                                           const float *__restrict__ table,
                                                           int32_t *__restrict__ col,
-                                                          float *__restrict__ val) {
+                                                          float *__restrict__ val,
+                                                          uint8_t *__restrict__ ids) {
     const int lane = threadIdx.x & 63;
     const int32_t waves = gridDim.x * (blockDim.x / 64);
     for (int32_t j = (blockIdx.x * blockDim.x + threadIdx.x) / 64; j < rows; j += waves) {
@@ -73,6 +77,7 @@ __global__ __launch_bounds__(256) void encode_rows_kernel(const uint8_t *__restr
                                              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 col[slot] = i;
                 val[slot] = table[id];
+                if (ids) ids[slot] = id;
             }
             o += __popcll(m);
         }
@@ -89,11 +94,11 @@ hipError_t launch_encode_count(const uint8_t *dm, int32_t rows, int32_t cols, in
         const int64_t blocks = std::min<int64_t>(((int64_t)rows + 3) / 4, 65535);
         if (blocks > 0)
             hipLaunchKernelGGL(encode_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dm, rows,
-                               cols, stride, T, cnt, nullptr, nullptr, nullptr, nullptr);
+                               cols, stride, T, cnt, nullptr, nullptr, nullptr, nullptr, nullptr);
     } else if (cols > 0 && n_chunks > 0) {
         hipLaunchKernelGGL(encode_cols_kernel, dim3((unsigned)((cols + 255) / 256), (unsigned)n_chunks),
                            dim3(256), 0, s, dm, rows, cols, stride, chunk_rows, T, cnt, nullptr,
-                           nullptr, nullptr, nullptr);
+                           nullptr, nullptr, nullptr, nullptr);
     }
     return hipGetLastError();
 }
@@ -101,16 +106,16 @@ hipError_t launch_encode_count(const uint8_t *dm, int32_t rows, int32_t cols, in
 hipError_t launch_encode_fill(const uint8_t *dm, int32_t rows, int32_t cols, int32_t stride,
                               bool trans, int32_t chunk_rows, int32_t n_chunks, uint8_t T,
                               const int32_t *offs, const float *table, int32_t *col, float *val,
-                              hipStream_t s) {
+                              uint8_t *ids, hipStream_t s) {
     if (trans) {
         const int64_t blocks = std::min<int64_t>(((int64_t)rows + 3) / 4, 65535);
         if (blocks > 0)
             hipLaunchKernelGGL(encode_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dm, rows,
-                               cols, stride, T, nullptr, offs, table, col, val);
+                               cols, stride, T, nullptr, offs, table, col, val, ids);
     } else if (cols > 0 && n_chunks > 0) {
         hipLaunchKernelGGL(encode_cols_kernel, dim3((unsigned)((cols + 255) / 256), (unsigned)n_chunks),
                            dim3(256), 0, s, dm, rows, cols, stride, chunk_rows, T, nullptr, offs,
-                           table, col, val);
+                           table, col, val, ids);
     }
     return hipGetLastError();
 }

@@ -255,7 +255,14 @@ hipError_t launch_encode_count(const uint8_t *dm, int32_t rows, int32_t cols, in
 hipError_t launch_encode_fill(const uint8_t *dm, int32_t rows, int32_t cols, int32_t stride,
                               bool trans, int32_t chunk_rows, int32_t n_chunks, uint8_t T,
                               const int32_t *offs, const float *table, int32_t *col, float *val,
-                              hipStream_t s);
+                              uint8_t *ids, hipStream_t s);
+// The reference encoding from a device CSR (refenc_dev.hip): encode_csr_ref's result and
+// return codes (encode.h), -5 on a HIP error (err).  d_ids: the terms' ids (then `table`
+// is the codebook they index), else ids from the values (table, or the derived codebook).
+struct EncodeResult;
+int encode_csr_ref_device(const int32_t *d_rp, const int32_t *d_col, const float *d_val, const uint8_t *d_ids,
+                          int64_t n_rows, int64_t n_cols, int64_t nnz, const float *table,
+                          int32_t table_size, EncodeResult &out, hipStream_t s, hipError_t &err);
 hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
                            const int32_t *col, int32_t *d_flag, hipStream_t s);
 // Dense decode: out is zeroed by the caller.  b_layout: out[row*stride+col]

@@ -632,6 +632,14 @@ def test_golden_device_encode(sm, name):
     assert (D.NumRows(), D.NumCols()) == (H.NumRows(), H.NumCols())
     for a, b in zip(H.csr(), D.csr()):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # The reference stream, encoded on the device from the index's ids (refenc_dev.hip):
+    # the compiled reference's bytes and panels (golden), so the two matrices are ==.
+    st = D.ref_stream()
+    assert np.array_equal(st["pos"], c.pos) and np.array_equal(st["val"], c.val)
+    assert np.array_equal(st["panel_col_off"], c.panel_col_off)
+    assert np.array_equal(st["panel_begin"], c.panel_begin)
+    assert np.array_equal(st["panel_end"], c.panel_end)
+    assert D == H
     if c.s_rows and c.s_cols:
         got = D.CopyTo(None, c.s_rows, sm.SblasTrans)[: c.s_cols * c.s_rows]
         assert bits_equal(got.reshape(c.s_cols, c.s_rows), c.dense_b())
@@ -658,6 +666,17 @@ def test_device_encode_random_matches_host(sm, trans, rows, cols, stride, dens, 
     for a, b in zip(H.csr(), D.csr()):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert D.info()["nnz"] == H.info()["nnz"]
+    sh, sd = H.ref_stream(), D.ref_stream()   # host encoder vs device encoder
+    for key in ("pos", "val", "panel_col_off", "panel_begin", "panel_end"):
+        assert np.array_equal(sh[key], sd[key]), key
+    # and the CSR-built route (sm_build_ref_stream, device sort) with the same codebook
+    R = sm.SparseMatrix.from_csr(*H.csr(), H.n_cols)
+    if T > 0 and D.info()["nnz"] > 0:
+        R.build_ref_stream(table)
+        sr = R.ref_stream()
+        assert np.array_equal(sr["pos"], sh["pos"]) and np.array_equal(sr["panel_begin"], sh["panel_begin"])
+        tb = np.concatenate([table, np.zeros(1, np.float32)]).view(np.uint32)
+        assert np.array_equal(tb[sr["val"]], tb[sh["val"]])
 
 
 @pytest.mark.parametrize("gband", [14, 15])
