@@ -76,7 +76,7 @@ constexpr int kCsellTabCopies = 4;
 constexpr int64_t kSellTsMax = 1 << 18;
 __device__ unsigned long long g_sell_ts[2 * kSellTsMax];
 #endif
-template <int U, bool TS = false, int ABL = 0, bool PIPE = true>
+template <int U, bool TS = false, int ABL = 0>
 __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
@@ -108,50 +108,7 @@ __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     const uint32_t *w = word + base + lane;
     const int cp = lane & (kCsellTabCopies - 1);
     constexpr uint32_t kColMask = (1u << kSellCbColBits) - 1u;
-    int32_t j = 0;
-    if (PIPE && L >= 4 * U) {
-        // Long slices (a lane walks up to 2048 slots): a chain of dependent memory round
-        // trips per group of U slots -- word load, then x gather -- made a few long waves
-        // the kernel's tail.  Software-pipelined: the words of group g+3 and the x values
-        // of group g+1 are in flight while group g is added (rings with static roles, four
-        // groups per iteration; loads past the slice read the next slice's slots or the
-        // layout's zero tail and are never added).
-        uint32_t W[4][U];
-        float XG[2][U], TV[2][U];
-        auto ld_w = [&](int32_t jj, uint32_t *dst) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) dst[u] = __builtin_nontemporal_load(w + (int64_t)(jj + u) * kSellLanes);
-        };
-        auto ld_x = [&](const uint32_t *src, float *xg, float *tv) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                xg[u] = x[(ABL & 1) ? 0u : (src[u] & kColMask)];
-                tv[u] = tab[(src[u] >> kSellCbColBits) * kCsellTabCopies + cp];
-            }
-        };
-        auto add = [&](int32_t jj, const float *xg, const float *tv) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float t = __fmul_rn(xg[u], tv[u]);
-                if (jj + u < n) acc = __fadd_rn(acc, t);
-            }
-        };
-        ld_w(0, W[0]);
-        ld_w(U, W[1]);
-        ld_w(2 * U, W[2]);
-        ld_x(W[0], XG[0], TV[0]);
-        const int32_t L4 = L & ~(4 * U - 1);   // whole iterations of four groups
-        for (; j < L4; j += 4 * U) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int32_t jj = j + k * U;
-                ld_w(jj + 3 * U, W[(k + 3) & 3]);
-                ld_x(W[(k + 1) & 3], XG[(k + 1) & 1], TV[(k + 1) & 1]);
-                add(jj, XG[k & 1], TV[k & 1]);
-            }
-        }
-    }
-    for (; j < L; j += U) {
+    for (int32_t j = 0; j < L; j += U) {
         uint32_t ww[U];
         float xg[U], tv[U];
 #pragma unroll
@@ -268,16 +225,7 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
                            sd.d_partials, alpha, beta);
         sell_ts_report(sd, s);
     } else if (sd.d_table) {
-        static const bool nopipe = [] {
-            const char *e = dev_env("SM_SELL_PIPE");
-            return e && atoi(e) == 0;
-        }();
         if (unroll == 16) SM_CSELL_K(16);
-        else if (nopipe)   // the round-3 loop (A/B)
-            hipLaunchKernelGGL((spmv_csell_kernel<8, false, 0, false>), dim3((unsigned)grid), dim3(kSellThreads),
-                               0, s, sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
-                               reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size, x, y,
-                               sd.d_partials, alpha, beta);
         else SM_CSELL_K(8);
     } else if (abl == 1) SM_SELL_K(8, 1);
     else if (unroll == 16) SM_SELL_K(16, 0);

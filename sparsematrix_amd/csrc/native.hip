@@ -36,7 +36,7 @@ constexpr int kNatThreads = 256;
 constexpr int kNatPer = 16;                          // entries per thread per batch
 constexpr int kNatBatch = kNatThreads * kNatPer;     // 4096
 constexpr int kNatCols = 64;                         // output columns per workgroup
-constexpr int kNs1MaxBatches = 16;                   // native_spmv_kernel: panels up to this long
+constexpr int kNs1MaxBatches = 4;                    // native_spmv_kernel: panels up to this long (r4: 1.2x faster on config 1, 1.1x slower at 9 batches)
 constexpr int kNatWords = 128;                       // bitmap words per column (4096 rows)
 constexpr int kNatStride = kNatWords + 4;            // word w of column c at c*132 + w + w/32:
                                                      // the 4 quarter readers of one column,

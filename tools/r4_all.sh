@@ -43,7 +43,7 @@ run_rehearse() {
 }
 run_rmat() {
   local rc
-  for v in "pipe|SM_SELL_TS=1" "nopipe|SM_SELL_TS=1 SM_SELL_PIPE=0" "pipe_nogather|SM_SELL_TS=1 SM_SELL_ABLATE=1"; do
+  for v in "ts|SM_SELL_TS=1" "nogather|SM_SELL_TS=1 SM_SELL_ABLATE=1"; do
     local nm=${v%%|*} ev=${v#*|}
     env SM_LIB_PATH=build/dev/libsparsematrix_amd.so $ev RMAT_PROF_REPS=2 timeout -k 10 300 python -u tools/rmat_prof.py > "$OUT/r4_rmat_$nm.log" 2>&1
     rc=$?
@@ -76,6 +76,15 @@ run_sellpipe() {   # the sell tests on the dev library, pipelined loop off and o
 }
 run_spmm() { prof spmm 300 python3 "$ROOT/tools/spmm_ab.py" --algos auto,mfma --n 32; }
 run_native() { prof native 300 python3 "$ROOT/tools/native_bench.py"; }
+run_nativeab() {   # m = 1: the counting-sort kernel (SM_NAT_SORT=1) vs the round-3 kernels (0), dev library
+  local rc
+  for v in 1 0 1 0; do
+    SM_LIB_PATH=$ROOT/build/dev/libsparsematrix_amd.so SM_NAT_SORT=$v timeout -k 10 200 python3 tools/native_bench.py > "$OUT/r4_nat$v.log" 2>&1
+    rc=$?
+    echo "-- SM_NAT_SORT=$v"; grep -E "^(config1|16384)" "$OUT/r4_nat$v.log"
+    [[ $rc -eq 0 ]] || return $rc
+  done
+}
 run_blas() {
   SBLAS_REPS=9 timeout -k 10 300 ./build/blas_test 1:32 16384 16384 0 "sgemm_sparse;sm_addmatmat_auto" > "$OUT/r4_blas.log" 2>&1
   local rc=$?
@@ -95,6 +104,7 @@ for s in "${ST[@]}"; do
     spmm) step spmm run_spmm ;;
     sellpipe) step sellpipe run_sellpipe ;;
     native) step native run_native ;;
+    nativeab) step nativeab run_nativeab ;;
     blas) step blas run_blas ;;
   esac
 done
