@@ -5,8 +5,10 @@ Workloads:
   config2 (default)  B is 2^20 x 2^20 per rank with exactly 16 distinct uniformly
                      random columns per row (fp32 values from a 255-entry codebook),
                      y = B x + 0.5 y with the library's AUTO layout.  N = 1: BASELINE
-                     config 2.  N > 1: weak scaling -- every rank owns 2^20 rows of an
-                     (N*2^20) x (N*2^20) matrix with global columns.
+                     config 2.  N > 1: weak scaling -- every rank owns a 2^20-row slab
+                     of an (N*2^20) x 2^20 matrix, i.e. exactly config 2's problem per
+                     GPU, x (2^20) all-gathered from N parts (`--square`: the round-3
+                     form, (N*2^20) x (N*2^20), whose per-rank x grows with N).
   config5            strong scaling: 2^26 x 2^26 (`--global-rows`), 16 columns per row,
                      rows split in N equal slices (8M rows x 64M columns per rank at
                      N = 8).  On one GPU, `--emulate-world W` builds rank 0's slice of a
@@ -181,6 +183,8 @@ def main():
     ap.add_argument("--rows-per-rank", type=int, default=1 << 20, help="config2")
     ap.add_argument("--global-rows", type=int, default=1 << 26, help="config5")
     ap.add_argument("--per-row", type=int, default=16)
+    ap.add_argument("--square", action="store_true",
+                    help="config2 N > 1: (N*2^20) x (N*2^20) instead of (N*2^20) x 2^20")
     ap.add_argument("--replicas", type=int, default=0, help="0: 4 (config2) / 1 (config5)")
     ap.add_argument("--replays", type=int, default=10,
                     help="N=1: extra graph replays for the per-SpMV time distribution")
@@ -245,7 +249,9 @@ def main():
     parts = world * emu
     if args.workload == "config2":
         R = args.rows_per_rank
-        C = R * parts                       # global columns (= global rows)
+        # Global columns: 2^20 (each rank's slab is config 2 itself; weak scaling of the
+        # distribution), or with --square the global row count.
+        C = R * parts if args.square else R
         seed0 = 2
         replicas = args.replicas or 4
     else:
@@ -593,7 +599,8 @@ def main():
             "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
             "scaling": "weak" if args.workload == "config2" else "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": workload, "rows_per_rank": R, "cols": C, "nnz_per_rank": nnz,
+            "config": {"workload": workload, "global_rows": R * parts, "rows_per_rank": R, "cols": C,
+                       "nnz_per_rank": nnz,
                        "per_row": per, "replicas": replicas, "algo": args.algo,
                        "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
                        "build_s": round(build_s, 1),
