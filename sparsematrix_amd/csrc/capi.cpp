@@ -1788,13 +1788,13 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         e = after_launch(e, s, "sm_addmatmat native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat native");
     }
-    if (algo != SM_ALGO_PARITY && m <= 4 && n < ((int64_t)1 << 18) && k > 0) {
+    if (algo != SM_ALGO_PARITY && m <= (algo == SM_ALGO_EXACT ? 2 : 4) && n < ((int64_t)1 << 18) && k > 0) {
         // A few right-hand sides on a matrix of few B rows: the row-panel kernel would give
         // each B row one thread (n threads, a fraction of the chip), while the SpMV layouts
         // spread a row's work -- and rows of A and C are contiguous (x = A row i, y = C row
         // i), so m SpMVs need no transposes.  Same algo, so EXACT keeps the reference's
-        // order.  blas_test 16384^2: m = 2 / 4 1.55 / 1.56 ms through the row panel vs
-        // 0.25 ms per SpMV.
+        // order.  blas_test 16384^2 (row panel vs m SpMVs): AUTO m = 2 / 4 1.55 / 1.56 vs
+        // 0.48 / 0.96 ms; EXACT (its SpMV 0.45 ms) m = 2 1.55 vs 0.91, m = 4 1.56 vs 1.81.
         for (int32_t i = 0; i < m; i++) {
             const sm_status st = sm_spmv(mat, alpha, a + (int64_t)i * lda, beta, c + (int64_t)i * ldc, algo, stream);
             if (st != SM_OK) return st;
