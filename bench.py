@@ -111,8 +111,8 @@ KERNELS = {"stream": "spmv_stream_kernel",
            "blocked": "spmv_xband_kernel (blocked band layout, slab combine fused)",
            "gather": "spmv_gband_kernel (column-ordered bands, x gathered, slab combine fused)",
            "band2": "spmv_band2_kernel (balanced bands, distributed slab combine)",
-           "cband": "spmv_band2_kernel<CB> (balanced bands of 4-byte codebook words, "
-                    "distributed slab combine)",
+           "cband": "spmv_band2_kernel<CB, dma3> (balanced bands of 4-byte codebook words, x staged "
+                    "by a loader wave's LDS-DMA, distributed slab combine)",
            "ccsell": "spmv_ccsell_kernel (column-chunked sorted sliced-ELL)",
            "gcb": "spmv_gcb_kernel (gathered chunk bands: 2016-term bands, x gathered, rows' sums in LDS)",
            "sweep": "spmv_sweep_kernel (column-swept 256-row blocks, one wavefront each)"}
@@ -192,7 +192,7 @@ def main():
     ap.add_argument("--layout", default="auto",
                     help="A/B: force the matrix layout (sm_build_opts.layout name, e.g. gcb, gather)")
     ap.add_argument("--band-tall", type=int, default=0,
-                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2) for the config-2 matrices")
+                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2, 4 dma3, 6 wide) for the config-2 matrices")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")

@@ -320,7 +320,8 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 // Builds into `d` the balanced bands of an n_rows x n_cols CSR (the matrix's own, or
 // the hot column prefix of a relabeled graph); `forced`: keep mostly-padding bands.
-// Geometry (sm_build_opts.band_tall): 0 = wide (the default), 1 = tall; development
+// Geometry (sm_build_opts.band_tall): 0 = the default (dma3 for codebook words, wide
+// otherwise), 1 = tall, 2 = half2, 4 = dma3, 6 = wide; development
 // builds also take 3 = wide3 for codebook values (three chunks per wave, 12160-column
 // windows, one table copy; config 2: 38.5 vs 37.2 us wide -- the table's bank conflicts
 // cost what the third fewer bands save: 36.1 vs 36.2 us with the lookup ablated).
@@ -329,7 +330,13 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                              int32_t geo_opt, int32_t slabs, bool forced) {
     const bool tall = geo_opt == 1;
     const bool half2 = geo_opt == 2 && kind == kXbCband;
-    const B2Geom geom = half2 ? kB2Half2Cb : !tall ? kB2Wide : kind == kXbCband ? kB2TallCb : kB2TallB2;
+    // Codebook words default to dma3 (a loader wave stages x: config 2 34.0-34.6 vs 36.9-37.1
+    // us for the wide geometry); band_tall = 6 keeps the wide one.
+    const int32_t geo_req = geo_opt;
+    if (geo_opt == 0 && kind == kXbCband) geo_opt = 4;
+    const bool dma3 = (geo_opt == 4 || geo_opt == 5) && kind == kXbCband;
+    const B2Geom geom = half2 ? kB2Half2Cb : dma3 ? (geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb) : !tall ? kB2Wide
+                      : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
@@ -345,9 +352,10 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     const bool wide3 = false;
 #endif
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
-    if (geo_opt == 2) {   // half2: codebook words only; otherwise the wide geometry
-        if (!cb) return SM_OK;
-        g = kB2Half2Cb;
+    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5) {   // half2 / dma3: codebook words only
+        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb;
+        else if (geo_req == 0) g = kB2Wide;   // no codebook: 8-byte entries, wide geometry
+        else return SM_OK;                    // a codebook-only geometry was asked for
     }
     // Bands are fixed slots of g.chunks() * 64 entries: where a slab's density leaves
     // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
@@ -358,7 +366,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
     };
     bool ok = fits(g);
-    if (!ok && g.cpw == 3) {   // wide3 did not fit: the two-chunk wide geometry
+    if (!ok && (g.cpw == 3 || g.chunks() == kB2Dma3Cb.chunks())) {   // wide3 / dma3 did not fit: wide
         g = kB2Wide;
         ok = fits(g);
     }

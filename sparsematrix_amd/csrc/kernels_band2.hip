@@ -87,6 +87,9 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_E_EARLY
 #define SM_E_EARLY 0
 #endif
+#ifndef SM_LD_PRIO
+#define SM_LD_PRIO 3
+#endif
 #ifndef SM_CB_RFIRST
 #define SM_CB_RFIRST 1
 #endif
@@ -117,9 +120,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
     constexpr bool TALL = GEO == 1;
-    static_assert((GEO != 2 && GEO != 3) || CB, "wide3 and half2 are cband geometries");
+    static_assert(GEO < 2 || CB, "wide3, half2 and dma3 are cband geometries");
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
-                                                       : GEO == 3 ? kB2Half2Cb : kB2Wide;
+                       : GEO == 3 ? kB2Half2Cb : GEO == 4 ? kB2Dma3Cb : GEO == 5 ? kB2Dma3tCb : kB2Wide;
+    // dma3: wave kLdWave stages the x windows (LDS-DMA, three buffers, two bands ahead) and
+    // the other waves apply -- no x ever passes through an applying wave's registers, and
+    // the loader's wait for its DMA is the only vmcnt wait on x (its queue holds nothing else).
+    constexpr bool kLd = GEO == 4 || GEO == 5;
+    constexpr int kLdWave = kB2Threads / 64 - 1;
     constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
     constexpr int W = G.window;
@@ -142,6 +150,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // only the AE-1 younger entry loads -- at least the 3 ops really pending then
     // (one entry load, the window's two DMA pieces) once AE >= 4: no extra stall.
     constexpr bool kDma = CB && GEO == 0 && SM_CB_DMA != 0;
+    constexpr int kXBuf = kLd ? 3 : 2;   // x window buffers in LDS
     static_assert(!kDma || SM_CB_DMA_EAHEAD >= 4, "DMA variant: hipcc's entry waits must not stall");
     constexpr int AX = kDma ? 1 : CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
     constexpr int AE = kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
@@ -154,10 +163,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     constexpr bool kRFirst = !kDma && !kEarly && SM_CB_RFIRST != 0 && !(ABL & 1);
     constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
     constexpr int U0 = AX > ER ? AX : ER;
-    constexpr int U = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
-    static_assert(U % AX == 0 && U % ER == 0 && U % 2 == 0, "ring sizes divide the unroll");
+    constexpr int UA = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
+    constexpr int U = kLd ? (ER % 3 == 0 ? 2 * ER : 6 * ER / (ER % 2 ? 1 : 2)) : UA;
+    static_assert(U % AX == 0 && U % ER == 0 && U % 2 == 0 && (!kLd || U % 3 == 0), "ring sizes divide the unroll");
     static_assert(W % 4 == 0 && XV * 4 * kB2Threads >= W, "float4 slots cover the window");
-    __shared__ __attribute__((aligned(16))) float xs[2][W];
+    __shared__ __attribute__((aligned(16))) float xs[kXBuf][W];
     // Wide band2: + a scratch slot per lane (dummy lanes write there).  The other
     // kinds write only live lanes and use the LDS nearly to the last byte: their
     // hand-off words live in the x buffers once the band loop is over.
@@ -171,7 +181,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     __shared__ float tab[CB ? 256 * kTabCopies : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    constexpr bool kProf = (ABL & 1024) != 0;
+    constexpr bool kProf = (ABL & 1024) != 0 && !kLd;
     [[maybe_unused]] constexpr bool kTs = (ABL & 2048) != 0;
 #ifdef SM_DEV
     if constexpr (kTs) {
@@ -214,7 +224,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t r0 = b * block_rows;
     const int32_t nr = min(block_rows, n_rows - r0);
     const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
-    constexpr uint32_t kBandBytes = CB ? 4096u * CPW : 16384u;   // entries of one band
+    constexpr uint32_t kBandBytes = CB ? 4u * 64u * (uint32_t)G.chunks() : 16384u;   // entries of one band
+    // Threads that hold entries (dma3: all but the loader wave, whose loads go past the range).
+    constexpr int kApplyThreads = CB ? 64 * G.chunks() / CPW : kB2Threads;
+    static_assert(kApplyThreads <= kB2Threads && kBandBytes % kApplyThreads == 0, "whole entry slots per lane");
     const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * (kBandBytes / 4), (uint64_t)nb * kBandBytes);
     // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi), read
     // by readlane; the window advances by 64 bands when the x loads reach its hi half.
@@ -268,6 +281,23 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 : "memory");
         }
     };
+    // dma3: the loader wave's LDS-DMA of window q into buffer buf, W / 256 pieces of 1 KiB
+    // (one wave-instruction each); only windows of the tile are issued.
+    auto dma_win = [&](int32_t c, int32_t buf) {   // c: the window's first column
+#pragma unroll
+        for (int m = 0; m < W / 256; ++m) {
+            const uint32_t voff = 4u * (uint32_t)(c + m * 256 + lane * 4);
+            const uint32_t lds = __builtin_amdgcn_readfirstlane(xs_lds + 4u * (uint32_t)(buf * W + m * 256));
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(x_src), "s"(lds)
+                : "memory");
+        }
+    };
+    static_assert(!kLd || W % 256 == 0, "dma3 windows are whole 1 KiB pieces");
     auto store_x = [&](int buf, const float4 *xr) {
 #pragma unroll
         for (int k = 0; k < XV; ++k) {
@@ -282,7 +312,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // {word 2w, word 2w+1} for this lane; past the tile: zeros = dummies.
     using EV = typename std::conditional<CB, typename std::conditional<CPW == 3, u32x3, u32x2>::type, u32x4>::type;
     auto load_e = [&](int32_t q) -> EV {
-        const uint32_t off = kBandBytes * (uint32_t)q + (kBandBytes / kB2Threads) * (uint32_t)tid;
+        const uint32_t off = (kApplyThreads < kB2Threads && tid >= kApplyThreads)
+                                 ? 0xFFFFFFF0u
+                                 : kBandBytes * (uint32_t)q + (kBandBytes / kApplyThreads) * (uint32_t)tid;
         if (ABL & 4) return EV{};
         if constexpr (CB && CPW == 3)
             return __builtin_amdgcn_raw_buffer_load_b96(e_src, off, 0, SM_ENT_AUX);
@@ -450,7 +482,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // pending at the loop header are in the order the loop's back edge leaves them.
     float4 X[AX][XV];
     EV E[ER];
-    if constexpr (kDma) {
+    const int32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+    if constexpr (kLd) {
+#pragma unroll
+        for (int v = 0; v < AE; ++v) E[v] = load_e(v);
+        if (wid == kLdWave) {   // windows 0 and 1; waited for (with everything) below
+            if (nb > 0) dma_win(clg[0], 0);
+            if (nb > 1) dma_win(clg[1], 1);
+        }
+    } else if constexpr (kDma) {
 #pragma unroll
         for (int v = 0; v < AE; ++v) E[v] = load_e(v);
         dma_x(0, 0);
@@ -521,7 +561,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         for (int q = 0; q < kQ; ++q)
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
-    if constexpr (!kDma) store_x(0, X[0]);
+    if constexpr (kLd) {
+        if (wid == kLdWave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (!kDma) {
+        store_x(0, X[0]);
+    }
     __syncthreads();
 #if SM_B2_EPOCH
     // The commit check's snapshot (xband_dev.h slab_handoff_epoch): read now, used after the
@@ -537,6 +581,43 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // scratch slots).
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
     mark_phase(0);
+    if constexpr (kLd) {
+        if (wid == kLdWave) {
+            // Band q: DMA window q+2 into the buffer window q-1 left (every wave passed
+            // band q-1's barrier), then wait until window q+1 has landed -- the 30 pieces
+            // just issued may stay in flight -- and meet the others at the barrier.
+            // The windows' first columns come by scalar loads one band ahead (a vector load
+            // here would make hipcc wait for the whole DMA queue before reading it).
+            int32_t c_next = nb > 2 ? clg[2] : 0;
+            __builtin_amdgcn_s_setprio(SM_LD_PRIO);   // the DMA issue goes first
+            for (int32_t q = 0; q < nb; ++q) {
+                if (q + 2 < nb) {
+                    const int32_t c = c_next;
+                    const int32_t qn = __builtin_amdgcn_readfirstlane(q + 3);
+                    if (qn < nb) c_next = clg[qn];
+                    dma_win(c, (q + 2) % 3);
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W / 256) : "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+            }
+        } else {
+            for (int32_t p = 0; p < nbu; p += U) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t q = p + u;
+                    if constexpr (ABL & 1) {
+                        asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
+                    } else {
+                        apply_cb(xs[u % 3], E[u % ER]);
+                    }
+                    E[u % ER] = load_e(q + AE);
+                    if (q < nb) __syncthreads();
+                }
+            }
+        }
+    } else
     for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -635,8 +716,11 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     const bool cb = xb.kind == kXbCband;
     const bool wide3 = cb && xb.band_cols == kB2Wide3Cb.window;
     const bool half2 = cb && xb.band_cols == kB2Half2Cb.window;
-    const bool tall = !wide3 && !half2 && xb.band_cols != kB2Wide.window;
-    const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+    const bool dma3 = cb && xb.band_cols == kB2Dma3Cb.window;
+    const bool dma3t = cb && xb.band_cols == kB2Dma3tCb.window;
+    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && xb.band_cols != kB2Wide.window;
+    const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? kB2Dma3Cb : dma3t ? kB2Dma3tCb
+                   : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -669,6 +753,20 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         case 0: SM_B2(0, 2, true, 3); break;
         case 8: SM_B2(8, 2, true, 3); break;
         case 2048: SM_B2(2048, 2, true, 3); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (dma3t) {
+        if (abl != 0) return hipErrorInvalidValue;
+        SM_B2(0, 2, true, 5);
+        return hipGetLastError();
+    }
+    if (dma3) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true, 4); break;
+        case 1: SM_B2(1, 2, true, 4); break;
+        case 8: SM_B2(8, 2, true, 4); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
@@ -779,6 +877,10 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (wide3) return hipErrorInvalidValue;   // development builds only
     if (half2) {
         SM_B2(0, 2, true, 3);
+    } else if (dma3) {
+        SM_B2(0, 2, true, 4);
+    } else if (dma3t) {
+        SM_B2(0, 2, true, 5);
     } else if (tall) {
         if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {

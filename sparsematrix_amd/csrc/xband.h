@@ -117,8 +117,9 @@ struct B2Geom {
     int32_t cpw = 2;          // chunks per wave per band
     int32_t cb_col = kCbColBits;   // cband column bits (row offset: 23 - cb_col bits)
     int32_t tab_copies = 32;  // cband: LDS copies of the scaled table (kernel)
+    int32_t nch = 0;          // chunks per band when not 16 * cpw (dma3: 15 applying waves)
     constexpr uint32_t dummy_word() const { return kB2DummyRank << col_bits; }
-    constexpr int chunks() const { return 16 * cpw; }
+    constexpr int chunks() const { return nch ? nch : 16 * cpw; }
     constexpr uint32_t cb_dummy_word() const { return kCbDummyId << cb_col; }
     constexpr int cb_off_shift() const { return cb_col + kCbIdBits; }
     constexpr uint32_t cb_off_mask() const { return (1u << (31 - kCbIdBits - cb_col)) - 1u; }
@@ -133,6 +134,12 @@ constexpr B2Geom kB2Wide3Cb{1 << 14, 12160, 14, 3, 14, 1};
 // (128 blocks x 2 = 256 tiles): twice the x per term of the wide geometry, but each tile hands
 // off half its sums to ONE sibling instead of three quarters to three.
 constexpr B2Geom kB2Half2Cb{1 << 13, 15872, 14, 2, 14, 4};
+// dma3 (cband only): wave 15 stages the x windows by LDS-DMA two bands ahead into three
+// 30 KiB buffers (7680 columns) and applies nothing; waves 0-14 apply chunks 2w, 2w+1 of
+// 30-chunk bands and never touch x in registers.  LDS: 3 x 30 KiB + 64 KiB + 4 table copies.
+constexpr B2Geom kB2Dma3Cb{1 << 14, 7680, 13, 2, 13, 4, 30};
+// dma3 with 7168-column windows: 4 KiB freed for 8 table copies (development A/B).
+constexpr B2Geom kB2Dma3tCb{1 << 14, 7168, 13, 2, 13, 8, 30};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

@@ -65,8 +65,11 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1])
+@pytest.mark.parametrize("tall", [0, 1, 6])
 def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
+    """tall: 0 the default (cband: dma3), 1 tall, 6 wide (band2: the same as 0)."""
+    if tall == 6 and kind == "band2":
+        pytest.skip("band2's default is the wide geometry")
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
     M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind, tall)
     if slabs == 1:
@@ -125,7 +128,7 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1])
+@pytest.mark.parametrize("tall", [0, 1, 6])
 def test_band2_special_values_and_signed_zeros(sm, kind, tall):
     n_rows, n_cols = 30000, 50000
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77,
@@ -153,7 +156,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1])
+@pytest.mark.parametrize("tall", [0, 1, 6])
 def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
@@ -201,6 +204,70 @@ def test_cband_half2_config2_vs_slab_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=2))
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_slabs"] == 2 and info["xband_block_rows"] == 8192, info
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.0, 0.5)
+    want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
+                           1.0, 0.5, info["xband_slab_cols"])
+    assert np.array_equal(bits(to_host(y)), bits(want))
+
+
+@pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
+def test_cband_dma3_vs_oracle(sm, n_rows, n_cols, per_row):
+    """The dma3 geometry (a loader wave stages 7680-column x windows by LDS-DMA into three
+    buffers, 15 waves apply 30-chunk bands): bit-identical to the slab-order oracle."""
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + 5 * n_cols)
+    for slabs in (1, None):
+        M, info = _band2(sm, rp, ci, va, n_cols, slabs, "cband", 4)
+        assert info["xband_block_rows"] <= 16384, info
+        rng = np.random.default_rng(9)
+        x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+        y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+        y0[::89] = np.nan
+        for alpha, beta in ((1.0, 0.5), (1.3, 0.0), (1.0, 1.0)):
+            _check(M, info, rp, ci, va, x, y0, alpha, beta)
+
+
+def test_cband_dma3_special_values_and_repeats(sm):
+    """dma3 with inf / NaN / -0.0 in values, x and y, unaligned windows past n_cols, and six
+    back-to-back launches (the hand-off's epoch words) all equal to the oracle."""
+    torch = torch_dev()
+    n_rows, n_cols = 300000, 400003
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=31,
+                             table=np.random.default_rng(2).uniform(-1, 1, 250).astype(np.float32))
+    va = va.copy()
+    va[::997] = np.inf
+    va[5::1009] = -0.0
+    M, info = _band2(sm, rp, ci, va, n_cols, None, "cband", 4)
+    assert info["xband_slabs"] > 1, info
+    rng = np.random.default_rng(32)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    x[1::4999] = -np.inf
+    x[2::7001] = np.nan
+    x[-1] = np.inf                     # the last column, inside the last window
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    y0[:300] = -0.0
+    want = slab_order_spmv(rp, ci, va, x, y0, 1.0, 0.5, info["xband_slab_cols"])
+    xd = to_dev(x)
+    ys = [to_dev(y0) for _ in range(6)]
+    for y in ys:
+        M.spmv(xd, y, 1.0, 0.5)
+    torch.cuda.synchronize()
+    for y in ys:
+        assert np.array_equal(bits(to_host(y)), bits(want))
+
+
+def test_cband_dma3_config2_vs_slab_oracle(sm):
+    """Config 2 in the dma3 geometry: bit-identical to the 4-slab restatement."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=4))
+    info = M.info()
+    assert info["has_xband"] == 5 and info["xband_block_rows"] == 16384, info
     g = torch.Generator(device="cuda").manual_seed(9)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
