@@ -15,6 +15,7 @@
 // ascend in column) every row's terms are added in the reference's order
 // (sparse-matrix.cc:164-190, kernel.cc:780-796: per output, ascending column).
 #include <algorithm>
+#include <cstdlib>
 #include <thread>
 
 #include "xband.h"
@@ -55,6 +56,17 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
     const uint32_t cb_colmask = (1u << geom.cb_col) - 1u, cb_dummy = geom.cb_dummy_word();
     const int cb_off_shift = geom.cb_off_shift();
     const bool tab_banks = cb && geom.tab_copies == 1;   // one table copy: bank = id mod 32
+    // Four table copies (dma3): lane l reads copy l mod 4, bank = 4 (id mod 8) + l mod 4 --
+    // the lane's class (l mod 4) matters, so singles are placed by (half, class).
+#ifdef SM_DEV
+    static const bool tab4_off = getenv("SM_B2_TAB4") && atoi(getenv("SM_B2_TAB4")) == 0;   // A/B
+#else
+    constexpr bool tab4_off = false;
+#endif
+    const bool tab4 = cb && geom.tab_copies == 4 && !tab4_off;
+    auto tbank = [&](uint32_t id, int lane) -> int {
+        return tab_banks ? (int)(id & 31) : tab4 ? (int)((4 * (id & 7) + (uint32_t)(lane & 3)) & 31) : 0;
+    };
     const int32_t base = segs.empty() ? 0 : segs.front().rl;   // segments come in row order
     int next = 0;
     // Bank use per half: x reads (column bank), accumulator reads (row bank) and, with
@@ -65,7 +77,7 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
         const int h = lane >> 5;
         xb[h][cbits & 31]++;
         if (!(same_row_before && ((lane - 1) >> 5) == h)) yb[h][rl & 31]++;
-        tb[h][id & 31]++;
+        tb[h][tbank(id, lane)]++;
     };
     if (cb) {
         const uint32_t h = ((uint32_t)base & cb_colmask) | cb_dummy |
@@ -123,6 +135,38 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
     int free_in[2] = {0, 0};
     for (int l = 0; l < 64; l++)
         if (!used[l]) free_in[l >> 5]++;
+    if (tab4) {
+        // (half, lane class) per single: x and accumulator banks by half as below, the
+        // table bank by half and class; then a free lane of that class in that half.
+        int free_hc[2][4] = {};
+        for (int l = 0; l < 64; l++)
+            if (!used[l]) free_hc[l >> 5][l & 3]++;
+        std::vector<uint8_t> cls((size_t)ns);
+        for (int i : order) {
+            const uint32_t id = ids[single[(size_t)i]->s];
+            int best = -1, bcls = 0, bcost = 1 << 30;
+            for (int h = 0; h < 2; h++)
+                for (int c = 0; c < 4; c++) {
+                    if (free_hc[h][c] == 0) continue;
+                    const int a = xb[h][sx[(size_t)i]] + 1, b = yb[h][sy[(size_t)i]] + 1;
+                    const int t = tb[h][tbank(id, c)] + 1;
+                    const int cost = 64 * (a * a + b * b + t * t) - free_hc[h][c];
+                    if (cost < bcost) { bcost = cost; best = h; bcls = c; }
+                }
+            half[(size_t)i] = (uint8_t)best;
+            cls[(size_t)i] = (uint8_t)bcls;
+            free_hc[best][bcls]--;
+            xb[best][sx[(size_t)i]]++;
+            yb[best][sy[(size_t)i]]++;
+            tb[best][tbank(id, bcls)]++;
+        }
+        for (int i = 0; i < ns; i++) {
+            int lane = 32 * half[(size_t)i] + cls[(size_t)i];
+            while (used[lane]) lane += 4;   // a free lane of the class exists (counted above)
+            put(*single[(size_t)i], 0, lane);
+        }
+        return;
+    }
     for (int i : order) {
         int best = -1, bcost = 1 << 30;
         for (int h = 0; h < 2; h++) {

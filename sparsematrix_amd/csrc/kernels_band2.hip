@@ -182,6 +182,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     constexpr bool kProf = (ABL & 1024) != 0 && !kLd;
+    // dma3 (ABL & 4096, development): cycles per band of every phase -- applying waves: the
+    // entry wait, the apply, the barrier; the loader: the DMA issue, its wait, the barrier.
+    constexpr bool kProfLd = (ABL & 4096) != 0 && kLd;
     [[maybe_unused]] constexpr bool kTs = (ABL & 2048) != 0;
 #ifdef SM_DEV
     if constexpr (kTs) {
@@ -189,9 +192,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
 #endif
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tk = kProf ? clock64() : 0;
+    unsigned long long tk = (kProf || kProfLd) ? clock64() : 0;
     auto mark_phase = [&](int k) {
-        if constexpr (kProf) {
+        if constexpr (kProf || kProfLd) {
             const unsigned long long now = clock64();
             ph[k] += now - tk;
             tk = now;
@@ -581,6 +584,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // scratch slots).
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
     mark_phase(0);
+    if constexpr (kProfLd) ph[0] = 0;   // the prologue is not a band phase
     if constexpr (kLd) {
         if (wid == kLdWave) {
             // Band q: DMA window q+2 into the buffer window q-1 left (every wave passed
@@ -595,25 +599,38 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                     const int32_t c = c_next;
                     const int32_t qn = __builtin_amdgcn_readfirstlane(q + 3);
                     if (qn < nb) c_next = clg[qn];
+                    if constexpr (kProfLd) mark_phase(5);
                     dma_win(c, (q + 2) % 3);
+                    if constexpr (kProfLd) mark_phase(3);
                     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W / 256) : "memory");
                 } else {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
+                if constexpr (kProfLd) mark_phase(4);
                 __syncthreads();
+                if constexpr (kProfLd) mark_phase(5);
             }
         } else {
             for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int32_t q = p + u;
+                    if constexpr (kProfLd) {
+                        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AE - 1) : "memory");
+                        mark_phase(0);
+                    }
                     if constexpr (ABL & 1) {
                         asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
                     } else {
                         apply_cb(xs[u % 3], E[u % ER]);
                     }
+                    if constexpr (kProfLd) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        mark_phase(1);
+                    }
                     E[u % ER] = load_e(q + AE);
                     if (q < nb) __syncthreads();
+                    if constexpr (kProfLd) mark_phase(2);
                 }
             }
         }
@@ -680,6 +697,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         }
         if constexpr (kProf) {
             mark_phase(5);
+            if (lane == 0)
+                for (int k = 0; k < 8; ++k) atomicAdd(&g_b2_prof[k], ph[k]);
+        }
+        if constexpr (kProfLd) {   // [6] bands, [7] applying waves (the loader adds 1 << 32)
+            ph[6] = (unsigned long long)nb;
+            ph[7] = wid == kLdWave ? (1ull << 32) : 1ull;
             if (lane == 0)
                 for (int k = 0; k < 8; ++k) atomicAdd(&g_b2_prof[k], ph[k]);
         }
@@ -762,8 +785,24 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         SM_B2(0, 2, true, 5);
         return hipGetLastError();
     }
-    if (dma3) {
+    if (dma3 && abl != 2048) {
         switch (abl) {
+        case 4096: {
+            unsigned long long h[8] = {};
+            void *sym = nullptr;
+            if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_prof)) != hipSuccess) return hipErrorInvalidValue;
+            (void)hipMemsetAsync(sym, 0, sizeof(h), s);
+            SM_B2(4096, 2, true, 4);
+            (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double wa = (double)(h[7] & 0xFFFFFFFFull), wl = (double)(h[7] >> 32);
+            const double bands = (double)h[6] / (wa + wl);
+            fprintf(stderr, "dma3 prof (cycles per band per wave; %.0f applying + %.0f loader waves, %.1f bands): "
+                    "apply waves: entry wait %.0f apply %.0f barrier %.0f | loader: issue %.0f dma wait %.0f "
+                    "barrier %.0f\n", wa, wl, bands, h[0] / wa / bands, h[1] / wa / bands, h[2] / wa / bands,
+                    h[3] / wl / bands, h[4] / wl / bands, h[5] / wl / bands);
+            break;
+        }
         case 0: SM_B2(0, 2, true, 4); break;
         case 1: SM_B2(1, 2, true, 4); break;
         case 8: SM_B2(8, 2, true, 4); break;
@@ -829,7 +868,8 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             std::vector<unsigned long long> h((size_t)3 * nt);
             void *sym = nullptr;
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
-            SM_B2(2048, 2, true, 0);
+            if (dma3) SM_B2(2048, 2, true, 4);
+            else SM_B2(2048, 2, true, 0);
             (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
             unsigned long long t0 = ~0ull;
