@@ -87,6 +87,9 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_E_EARLY
 #define SM_E_EARLY 0
 #endif
+#ifndef SM_LD_TPF
+#define SM_LD_TPF 0
+#endif
 #ifndef SM_LD_PRIO
 #define SM_LD_PRIO 3
 #endif
@@ -418,7 +421,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         uint32_t rl[CPW];
         uint64_t live[CPW], cont[CPW];
     };
-    auto cb_read = [&](const float *xb, EV e) -> CbState {
+    // The codebook values of a band's two chunks (dma3 reads them a band early, TPF).
+    auto tab_read = [&](EV e, float *tv) {
+#pragma unroll
+        for (int k = 0; k < CPW; ++k) {
+            const uint32_t id = ((e[k] ^ kCbDummy) >> G.cb_col) & kCbDummyId;
+            tv[k] = tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+        }
+    };
+    auto cb_read = [&](const float *xb, EV e, const float *tv_pre = nullptr) -> CbState {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
         CbState st;
 #pragma unroll
@@ -431,7 +442,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             st.cont[k] = __ballot((int32_t)wd < 0);
             st.rl[k] = base + ((wd >> kCbOffSh) & kCbOffM);
             st.xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd & kCbCol)];
-            st.tv[k] = (ABL & 32) ? __uint_as_float(id) : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+            st.tv[k] = (ABL & 32) ? __uint_as_float(id)
+                       : tv_pre ? tv_pre[k] : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
             st.yv[k] = yacc[st.rl[k]];
         }
         return st;
@@ -611,6 +623,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 if constexpr (kProfLd) mark_phase(5);
             }
         } else {
+            // TPF (SM_LD_TPF=1, development A/B): band q+1's codebook values read during band q,
+            // so after each barrier only the x and accumulator reads queue on the LDS -- measured
+            // slower (35.5 vs 34.1 us: its wait for band q+1's entries, one band after their load).
+            constexpr bool kTpf = SM_LD_TPF != 0;
+            float tvn[CPW];
+            if constexpr (kTpf) tab_read(E[0], tvn);
             for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -621,6 +639,13 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                     }
                     if constexpr (ABL & 1) {
                         asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
+                    } else if constexpr (kTpf) {
+                        // band q's reads, then band q+1's codebook reads behind them (they
+                        // land while band q adds), then band q's adds and writes
+                        const CbState st = cb_read(xs[u % 3], E[u % ER], tvn);
+                        asm volatile("" ::: "memory");   // keep band q's reads first in the LDS queue
+                        tab_read(E[(u + 1) % ER], tvn);
+                        cb_finish(st);
                     } else {
                         apply_cb(xs[u % 3], E[u % ER]);
                     }
