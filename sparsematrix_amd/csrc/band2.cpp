@@ -191,8 +191,78 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
     }
 }
 
+// Cross-chunk balance (codebook bands): a band's chunks are cut in row order, so each single
+// term could also sit in a neighbouring chunk whose rows stay within the row span.  Swapping
+// singles between neighbours so each chunk's x banks (column mod 32) and accumulator banks
+// (row mod 32) repeat less gives emit_chunk's half / lane-class placement a better start:
+// the per-half read costs it reaches fall with the chunk-level sums of squared bank counts.
+// Rows move between chunks only (each row is still one segment of one chunk), so the sums
+// are unchanged.  Singles whose banks repeat at least `hot` times are the candidates.
+void balance_chunks(std::vector<std::vector<Seg>> &cs, int nc, const int32_t *col, int32_t clo_al,
+                    int32_t span) {
+    struct Ch {
+        uint8_t cx[32], cy[32];
+        int32_t mn, mn2, mx, mx2;   // two smallest / largest rows
+    };
+    std::vector<Ch> ch((size_t)nc);
+    auto xb = [&](const Seg &g) { return (int)((col[g.s] - clo_al) & 31); };
+    auto stats = [&](int c) {
+        Ch &h = ch[(size_t)c];
+        std::fill(h.cx, h.cx + 32, 0);
+        std::fill(h.cy, h.cy + 32, 0);
+        h.mn = h.mn2 = INT32_MAX;
+        h.mx = h.mx2 = INT32_MIN;
+        for (const Seg &g : cs[(size_t)c]) {
+            for (int32_t j = 0; j < g.n; j++) h.cx[(col[g.s + j] - clo_al) & 31]++;
+            h.cy[g.rl & 31]++;
+            if (g.rl < h.mn) { h.mn2 = h.mn; h.mn = g.rl; } else if (g.rl < h.mn2) h.mn2 = g.rl;
+            if (g.rl > h.mx) { h.mx2 = h.mx; h.mx = g.rl; } else if (g.rl > h.mx2) h.mx2 = g.rl;
+        }
+    };
+    for (int c = 0; c < nc; c++) stats(c);
+    constexpr int hot = 3;
+    for (int a = 0; a + 1 < nc; a++) {
+        const int b = a + 1;
+        for (int it = 0; it < 16; it++) {
+            Ch &A = ch[(size_t)a], &B = ch[(size_t)b];
+            int best_i = -1, best_j = -1, best = 0;
+            for (int i = 0; i < (int)cs[(size_t)a].size(); i++) {
+                const Seg &s_ = cs[(size_t)a][(size_t)i];
+                if (s_.n != 1) continue;
+                const int xs = xb(s_), ys = s_.rl & 31;
+                if (A.cx[xs] < hot && A.cy[ys] < hot) continue;
+                const int32_t amn = s_.rl == A.mn ? A.mn2 : A.mn, amx = s_.rl == A.mx ? A.mx2 : A.mx;
+                for (int j = 0; j < (int)cs[(size_t)b].size(); j++) {
+                    const Seg &t = cs[(size_t)b][(size_t)j];
+                    if (t.n != 1) continue;
+                    const int xt = xb(t), yt = t.rl & 31;
+                    // spans after the swap
+                    const int32_t bmn = t.rl == B.mn ? B.mn2 : B.mn, bmx = t.rl == B.mx ? B.mx2 : B.mx;
+                    if (std::max(amx, t.rl) - std::min(amn, t.rl) >= span) continue;
+                    if (std::max(bmx, s_.rl) - std::min(bmn, s_.rl) >= span) continue;
+                    int d = 0;   // change of the sums of squares (x and y, both chunks)
+                    if (xs != xt) d += 2 * (A.cx[xt] - A.cx[xs] + 1) + 2 * (B.cx[xs] - B.cx[xt] + 1);
+                    if (ys != yt) d += 2 * (A.cy[yt] - A.cy[ys] + 1) + 2 * (B.cy[ys] - B.cy[yt] + 1);
+                    if (d < best) { best = d; best_i = i; best_j = j; }
+                }
+            }
+            if (best_i < 0) break;
+            std::swap(cs[(size_t)a][(size_t)best_i], cs[(size_t)b][(size_t)best_j]);
+            stats(a);
+            stats(b);
+        }
+    }
+    for (int c = 0; c < nc; c++)   // emit_chunk: segments in row order, the first is the base
+        std::sort(cs[(size_t)c].begin(), cs[(size_t)c].end(), [](const Seg &x, const Seg &y) { return x.rl < y.rl; });
+}
+
 void build_tile(const int32_t *rp, const int32_t *col, const float *val, const uint8_t *ids,
                 int64_t r0, int64_t r1, int64_t c0, int64_t c1, B2Geom geom, TileOut &out) {
+#ifdef SM_DEV
+    static const bool kBalance = !(getenv("SM_B2_BAL") && atoi(getenv("SM_B2_BAL")) == 0);   // A/B
+#else
+    constexpr bool kBalance = true;
+#endif
     const int64_t nr = r1 - r0;
     const bool cb = ids != nullptr;
     // Chunk capacity, longest segment and row span of one chunk.
@@ -288,6 +358,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
             cur[(size_t)g.rl] += g.n;
             out.terms += g.n;
         }
+        if (cb && kBalance) balance_chunks(chunk_segs, c + 1, col, (int32_t)clo_al, span);
         for (int k = 0; k <= c; k++)
             emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al, geom);
         if (!split) clo = chi;   // split: the column's remaining rows go to the next band
