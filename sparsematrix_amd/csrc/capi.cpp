@@ -81,6 +81,7 @@ void free_xband_dev(XbandDev &h) {
     (void)hipFree(h.d_tickets);
     (void)hipFree(h.d_band_clo);
     (void)hipFree(h.d_table);
+    (void)hipFree(h.d_pace);
     h = XbandDev();
 }
 
@@ -438,6 +439,11 @@ static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col,
         SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)gh.n_blocks, m->device_bytes));
         SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)gh.n_blocks * 4 * sizeof(int32_t)));
     }
+    // Column pacing (kernels_gcb.hip): per dispatch group, a started count and one arrival
+    // count per 2^18-column checkpoint, monotonic across launches.
+    d.pace_k = (int32_t)((m->n_cols + kGcbMaxWindow - 1) / kGcbMaxWindow);
+    SM_TRY_HIP(dev_alloc(&d.d_pace, 8 * (1 + (int64_t)d.pace_k), m->device_bytes));
+    SM_TRY_HIP(hipMemset(d.d_pace, 0, (size_t)8 * (1 + d.pace_k) * sizeof(int32_t)));
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, gh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
                          hipMemcpyHostToDevice));
     if (gh.n_bands > 0) {

@@ -31,12 +31,14 @@ constexpr int kGcbThreads = 1024;
 
 // ABL (development builds, SM_GCB_ABLATE; results wrong): 1 no x gathers (x read as 0,
 // no memory request), 2 no apply (the loaded values kept live), 4 no per-band barrier.
-template <int ROWS_LOG2, int ER, int GA, int ABL = 0>
+// PACE: column pacing (below), a development A/B until measured.
+template <int ROWS_LOG2, int ER, int GA, int ABL = 0, bool PACE = false>
 __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ x, float *__restrict__ y,
-    float *__restrict__ partials, int32_t *__restrict__ ctl, float alpha, float beta) {
+    float *__restrict__ partials, int32_t *__restrict__ ctl, float alpha, float beta,
+    int32_t *__restrict__ pace, int32_t pace_k, int32_t pace_slack) {
     constexpr int BROWS = 1 << ROWS_LOG2;
     constexpr int XR = GA + 1;                  // x-value ring: band p's slot is not refilled at p
     constexpr int U = ER % XR == 0 ? ER : ER * XR;   // unroll: static ring roles
@@ -50,6 +52,20 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
     const int32_t b = t / n_slabs;
     const int32_t slab = t - b * n_slabs;
     handoff_started(ctl + (int64_t)b * kCtlWords, n_slabs);
+    // Column pacing (pace != null): the tiles of one dispatch group (blockIdx mod 8: one XCD
+    // under round-robin dealing, for speed only) sweep the columns together, so the x lines
+    // one tile gathers are still in the XCD's L2 when the group's other tiles reach them.  A
+    // tile adds 1 to checkpoint k's counter when its bands pass column k * 2^18, and before
+    // going past checkpoint k waits until every STARTED tile of its group has passed
+    // k - slack -- the slowest tile never waits, so the group always progresses.  Counters
+    // are monotonic across launches (launches on a matrix are ordered): this launch's counts
+    // are the values minus gen_base = launch index * group size.
+    const int32_t pg = (int32_t)(blockIdx.x & 7u);
+    const int32_t pn = ((int32_t)gridDim.x - pg + 7) / 8;   // tiles in the group
+    int32_t *pw = PACE ? pace + (int64_t)pg * (1 + pace_k) : nullptr;
+    int32_t gen_base = 0, kdone = -1;
+    if (PACE && tid == 0)
+        gen_base = __hip_atomic_fetch_add(pw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / pn * pn;
     const int32_t g0 = tile_band_start[t];
     const int32_t nb = tile_band_start[t + 1] - g0;
     const int32_t r0 = b * block_rows;
@@ -185,6 +201,21 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
         for (int u = 0; u < U; ++u) {
             const int32_t q = p + u;
             if (q + GA >= cw + 64) advance();   // the gather below reads clo of band q + GA
+            if (PACE && tid == 0 && q + GA < nb) {   // checkpoints passed by the band gathered next
+                const int32_t kq = min(clo_at(q + GA) >> kGcbColBits, pace_k - 1);
+                for (int32_t k = kdone + 1; k <= kq; ++k)
+                    __hip_atomic_fetch_add(pw + 1 + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (kq > kdone && kq >= pace_slack) {
+                    const int32_t kw = kq - pace_slack;
+                    for (;;) {
+                        const int32_t st = min(pn, __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - gen_base);
+                        const int32_t ar = __hip_atomic_load(pw + 1 + kw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - gen_base;
+                        if (ar >= st) break;
+                        __builtin_amdgcn_s_sleep(8);
+                    }
+                }
+                kdone = max(kdone, kq);
+            }
             gather(q + GA, E[(u + GA) % ER], XV[(u + GA) % XR]);
             if constexpr (ABL & 2) {
                 asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y), "v"(E[u % ER].z), "v"(E[u % ER].w),
@@ -197,6 +228,11 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
         }
     }
 
+    if (PACE && tid < 64) {   // every checkpoint not yet passed, so the counts stay per launch
+        const int32_t kd = __builtin_amdgcn_readfirstlane(kdone);
+        for (int32_t k = kd + 1 + tid; k < pace_k; k += 64)
+            __hip_atomic_fetch_add(pw + 1 + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (n_slabs == 1) {
         const int32_t nv = y_vec ? (nr & ~3) : 0;   // float4 rows, then the rest
 #pragma unroll
@@ -224,20 +260,26 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
 #define SM_GCB(RL, ER, GA)                                                                         \
     hipLaunchKernelGGL((spmv_gcb_kernel<RL, ER, GA>), grid, block, 0, s, n_rows, n_cols, xb.block_rows, \
                        xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
-                       xb.d_tickets, alpha, beta)
+                       xb.d_tickets, alpha, beta, pace, xb.pace_k, pace_slack)
     int look = 0;
+    int32_t *pace = nullptr;
+    int32_t pace_slack = 0;
     const bool tall = xb.block_rows > (1 << 14);
 #ifdef SM_DEV
     if (const char *e = dev_env("SM_GCB_LOOK")) look = atoi(e);   // development A/B of ER/GA
+    if (const char *e = dev_env("SM_GCB_PACE")) {   // column pacing, slack in checkpoints (A/B)
+        pace_slack = atoi(e);
+        if (pace_slack > 0 && xb.d_pace) pace = xb.d_pace;
+    }
     if (const char *e = dev_env("SM_GCB_ABLATE")) {
         const int abl = atoi(e);
 #define SM_GCBA(A)                                                                                    \
     if (tall) hipLaunchKernelGGL((spmv_gcb_kernel<15, 6, 2, A>), grid, block, 0, s, n_rows, n_cols, xb.block_rows, \
                                  xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
-                                 xb.d_tickets, alpha, beta);                                         \
+                                 xb.d_tickets, alpha, beta, pace, xb.pace_k, pace_slack);            \
     else hipLaunchKernelGGL((spmv_gcb_kernel<14, 6, 2, A>), grid, block, 0, s, n_rows, n_cols, xb.block_rows, \
                             xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,  \
-                            xb.d_tickets, alpha, beta)
+                            xb.d_tickets, alpha, beta, pace, xb.pace_k, pace_slack)
         switch (abl) {
         case 1: SM_GCBA(1); break;
         case 2: SM_GCBA(2); break;
@@ -250,6 +292,17 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
         return hipGetLastError();
     }
 #endif
+    if (pace) {
+        if (tall)
+            hipLaunchKernelGGL((spmv_gcb_kernel<15, 6, 2, 0, true>), grid, block, 0, s, n_rows, n_cols, xb.block_rows,
+                               xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,
+                               xb.d_tickets, alpha, beta, pace, xb.pace_k, pace_slack);
+        else
+            hipLaunchKernelGGL((spmv_gcb_kernel<14, 6, 2, 0, true>), grid, block, 0, s, n_rows, n_cols, xb.block_rows,
+                               xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y, xb.d_partials,
+                               xb.d_tickets, alpha, beta, pace, xb.pace_k, pace_slack);
+        return hipGetLastError();
+    }
     switch (look) {
     case 42: if (tall) SM_GCB(15, 4, 2); else SM_GCB(14, 4, 2); break;
     case 63: if (tall) SM_GCB(15, 6, 3); else SM_GCB(14, 6, 3); break;

@@ -86,6 +86,9 @@ struct XbandDev {
     // cband kind: the codebook (table_size <= 255 floats) the entries' ids index.
     float *d_table = nullptr;
     int32_t table_size = 0;
+    // gcb kind: column pacing words (kernels_gcb.hip), 8 x (1 + pace_k) monotonic counters.
+    int32_t *d_pace = nullptr;
+    int32_t pace_k = 0;
 };
 
 // Device copy of the sorted sliced-ELL layout (sell.h).
