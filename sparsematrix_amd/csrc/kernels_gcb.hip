@@ -32,7 +32,8 @@ constexpr int kGcbThreads = 1024;
 // ABL (development builds, SM_GCB_ABLATE; results wrong): 1 no x gathers (x read as 0,
 // no memory request), 2 no apply (the loaded values kept live), 4 no per-band barrier.
 // PACE: column pacing (below), a development A/B until measured.
-template <int ROWS_LOG2, int ER, int GA, int ABL = 0, bool PACE = false>
+// XAUX: cache-policy bits of the x gathers (development A/B).
+template <int ROWS_LOG2, int ER, int GA, int ABL = 0, bool PACE = false, int XAUX = 0>
 __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
     int32_t n_rows, int32_t n_cols, int32_t block_rows, int32_t n_slabs,
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kGcbThreads) void spmv_gcb_kernel(
             const uint32_t w = e[k];
             const uint32_t off = ((w & kGcbLive) && !(ABL & 1)) ? 4u * (uint32_t)(c + (int32_t)(w & kGcbColMask))
                                                                 : 0xFFFFFFF0u;
-            xv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x_src, off, 0, 0));
+            xv[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(x_src, off, 0, XAUX));
         }
     };
     auto shr1 = [](float v) {   // lane i <- lane i-1
@@ -267,6 +268,25 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
     const bool tall = xb.block_rows > (1 << 14);
 #ifdef SM_DEV
     if (const char *e = dev_env("SM_GCB_LOOK")) look = atoi(e);   // development A/B of ER/GA
+    if (const char *e = dev_env("SM_GCB_XAUX")) {   // x gather cache policy (A/B)
+        const int a = atoi(e);
+#define SM_GCBX(A)                                                                                 \
+    if (tall) hipLaunchKernelGGL((spmv_gcb_kernel<15, 6, 2, 0, false, A>), grid, block, 0, s, n_rows, n_cols,    \
+                                 xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y,  \
+                                 xb.d_partials, xb.d_tickets, alpha, beta, nullptr, 0, 0);                   \
+    else hipLaunchKernelGGL((spmv_gcb_kernel<14, 6, 2, 0, false, A>), grid, block, 0, s, n_rows, n_cols,         \
+                            xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word, x, y,       \
+                            xb.d_partials, xb.d_tickets, alpha, beta, nullptr, 0, 0)
+        switch (a) {
+        case 1: SM_GCBX(1); break;
+        case 2: SM_GCBX(2); break;
+        case 16: SM_GCBX(16); break;
+        case 17: SM_GCBX(17); break;
+        default: SM_GCBX(0); break;
+        }
+#undef SM_GCBX
+        return hipGetLastError();
+    }
     if (const char *e = dev_env("SM_GCB_PACE")) {   // column pacing, slack in checkpoints (A/B)
         pace_slack = atoi(e);
         if (pace_slack > 0 && xb.d_pace) pace = xb.d_pace;
