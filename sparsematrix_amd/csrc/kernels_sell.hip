@@ -76,7 +76,8 @@ constexpr int kCsellTabCopies = 4;
 constexpr int64_t kSellTsMax = 1 << 18;
 __device__ unsigned long long g_sell_ts[2 * kSellTsMax];
 #endif
-template <int U, bool TS = false, int ABL = 0>
+// XAUX (development A/B, SM_SELL_XAUX): cache-policy bits of the x gathers (buffer loads).
+template <int U, bool TS = false, int ABL = 0, int XAUX = -1>
 __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
     int64_t n_slices, const int64_t *__restrict__ off, const int32_t *__restrict__ len,
     const int32_t *__restrict__ row, const int32_t *__restrict__ row_len,
@@ -115,7 +116,13 @@ __global__ __launch_bounds__(kSellThreads) void spmv_csell_kernel(
         for (int u = 0; u < U; ++u) ww[u] = __builtin_nontemporal_load(w + (int64_t)(j + u) * kSellLanes);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            xg[u] = x[(ABL & 1) ? 0u : (ww[u] & kColMask)];
+            const uint32_t xi = (ABL & 1) ? 0u : (ww[u] & kColMask);
+            if constexpr (XAUX < 0)
+                xg[u] = x[xi];
+            else
+                xg[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x), (short)0, (int)0x7FFFFFFF, 0x00020000),
+                    4u * xi, 0, XAUX));
             tv[u] = tab[(ww[u] >> kSellCbColBits) * kCsellTabCopies + cp];
         }
 #pragma unroll
@@ -212,6 +219,28 @@ hipError_t launch_spmv_sell(const SellDev &sd, const float *x, float *y, float a
         return e ? atoi(e) : 8;
     }();
     static const bool ts = dev_env("SM_SELL_TS") != nullptr;
+    static const int xaux = [] {
+        const char *e = dev_env("SM_SELL_XAUX");
+        return e ? atoi(e) : -1;
+    }();
+    if (sd.d_table && xaux >= 0 && abl == 0 && !ts) {
+#define SM_CSELLX(A)                                                                                      \
+    hipLaunchKernelGGL((spmv_csell_kernel<8, false, 0, A>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,   \
+                       sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,                               \
+                       reinterpret_cast<const uint32_t *>(sd.d_col), sd.d_table, sd.table_size, x, y,          \
+                       sd.d_partials, alpha, beta)
+        switch (xaux) {
+        case 1: SM_CSELLX(1); break;
+        case 2: SM_CSELLX(2); break;
+        case 16: SM_CSELLX(16); break;
+        case 17: SM_CSELLX(17); break;
+        default: SM_CSELLX(0); break;
+        }
+#undef SM_CSELLX
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return launch_long_finalize(sd.n_long, sd.d_long_rows, sd.d_long_ptr, sd.d_partials, y, beta, s);
+    }
     if (sd.d_table && abl == 1) {   // the gathers ablated (one broadcast address), with the timeline
         hipLaunchKernelGGL((spmv_csell_kernel<8, true, 1>), dim3((unsigned)grid), dim3(kSellThreads), 0, s,
                            sd.n_slices, sd.d_off, sd.d_len, sd.d_row, sd.d_row_len,
