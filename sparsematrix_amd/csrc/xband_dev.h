@@ -99,9 +99,10 @@ __device__ __forceinline__ void combine_rows(const float *yacc, float *y, const 
         for (int32_t s0 = 0; s0 < n_slabs; s0 += 4) {
             u32x4 pv[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 4; ++j) {   // the own slab's part comes from LDS: no request
                 const int32_t s = min(s0 + j, n_slabs - 1);
-                pv[j] = __builtin_amdgcn_raw_buffer_load_b128(src(s), 4u * i, 0, kAuxSc1);
+                const uint32_t off = (s == me || s0 + j >= n_slabs) ? 0xFFFFFFF0u : 4u * (uint32_t)i;
+                pv[j] = __builtin_amdgcn_raw_buffer_load_b128(src(s), off, 0, kAuxSc1);
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
