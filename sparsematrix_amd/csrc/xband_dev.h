@@ -22,6 +22,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 constexpr int kAuxSc1 = 16; // write-through store / L1-bypassing load (cross-CU hand-off)
+#ifndef SM_COMBINE_SKIP_OWN
+#define SM_COMBINE_SKIP_OWN 1   // the slab combine issues no load for the own slab's part
+#endif
 
 // vmcnt retires in issue order: waiting until only the N most recent vector loads
 // are outstanding retires every older one, including LDS-DMA that hipcc does not count.
@@ -101,7 +104,8 @@ __device__ __forceinline__ void combine_rows(const float *yacc, float *y, const 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {   // the own slab's part comes from LDS: no request
                 const int32_t s = min(s0 + j, n_slabs - 1);
-                const uint32_t off = (s == me || s0 + j >= n_slabs) ? 0xFFFFFFF0u : 4u * (uint32_t)i;
+                const uint32_t off = (SM_COMBINE_SKIP_OWN && (s == me || s0 + j >= n_slabs)) ? 0xFFFFFFF0u
+                                                                                               : 4u * (uint32_t)i;
                 pv[j] = __builtin_amdgcn_raw_buffer_load_b128(src(s), off, 0, kAuxSc1);
             }
 #pragma unroll
