@@ -269,8 +269,8 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
     const int cap = cb ? kCbChunkTerms : 64;
     const int32_t max_seg = cb ? kCbChunkTerms : (int32_t)kB2DummyRank - 1;
     const int32_t span = cb ? geom.cb_row_span() : INT32_MAX;
-    const int nchunks = cb ? geom.chunks() : kB2Chunks;
-    const size_t band_words = cb ? (size_t)64 * nchunks : 4096;
+    const int nchunks = geom.chunks();   // band2's default: kB2Chunks (32)
+    const size_t band_words = (size_t)(cb ? 64 : 128) * nchunks;
     // A new chunk opens when the segment does not fit the current one (terms or rows).
     auto opens = [&](int fill, int32_t base, const Seg &g) {
         return fill + g.n > cap || g.rl - base >= span;
@@ -358,7 +358,7 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
             cur[(size_t)g.rl] += g.n;
             out.terms += g.n;
         }
-        if (cb && kBalance) balance_chunks(chunk_segs, c + 1, col, (int32_t)clo_al, span);
+        if (kBalance) balance_chunks(chunk_segs, c + 1, col, (int32_t)clo_al, span);
         for (int k = 0; k <= c; k++)
             emit_chunk(out.ent.data() + base, k, chunk_segs[(size_t)k], col, val, ids, (int32_t)clo_al, geom);
         if (!split) clo = chi;   // split: the column's remaining rows go to the next band
@@ -379,7 +379,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
         geom.block_rows > ((int64_t)1 << (32 - geom.col_bits - kB2RankBits)) ||
         geom.block_rows > ((int64_t)1 << (31 - kCbIdBits)))
         return false;
-    const int64_t band_words = ids ? (int64_t)64 * geom.chunks() : 4096;
+    const int64_t band_words = (int64_t)(ids ? 64 : 128) * geom.chunks();
     if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)

@@ -335,8 +335,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // us for the wide geometry); band_tall = 6 keeps the wide one.
     const int32_t geo_req = geo_opt;
     if (geo_opt == 0 && kind == kXbCband) geo_opt = 4;
-    const bool dma3 = (geo_opt == 4 || geo_opt == 5) && kind == kXbCband;
-    const B2Geom geom = half2 ? kB2Half2Cb : dma3 ? (geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb) : !tall ? kB2Wide
+    const bool dma3 = geo_opt == 4 || (geo_opt == 5 && kind == kXbCband);
+    const B2Geom geom = half2 ? kB2Half2Cb : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
+                      : !tall ? kB2Wide
                       : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
@@ -356,6 +357,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5) {   // half2 / dma3: codebook words only
         if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb;
         else if (geo_req == 0) g = kB2Wide;   // no codebook: 8-byte entries, wide geometry
+        else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
         else return SM_OK;                    // a codebook-only geometry was asked for
     }
     // Bands are fixed slots of g.chunks() * 64 entries: where a slab's density leaves
@@ -373,7 +375,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     }
     if (!ok) return SM_OK;
     std::vector<uint8_t>().swap(ids);
-    const int64_t band_words = cb ? (int64_t)64 * g.chunks() : 4096;
+    const int64_t band_words = (int64_t)(cb ? 64 : 128) * g.chunks();
     const int64_t ntile = (int64_t)bh.n_blocks * bh.n_slabs;
     SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, bh.n_bands), m->device_bytes));
@@ -406,7 +408,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_bands = (int32_t)std::min<int64_t>(bh.n_bands, INT32_MAX);
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
-    d.n_chunks = bh.n_bands * (cb ? g.chunks() : kB2Chunks);
+    d.n_chunks = bh.n_bands * g.chunks();
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
     return SM_OK;

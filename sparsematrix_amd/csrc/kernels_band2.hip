@@ -123,9 +123,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
     constexpr bool TALL = GEO == 1;
-    static_assert(GEO < 2 || CB, "wide3, half2 and dma3 are cband geometries");
+    static_assert(GEO < 2 || GEO == 4 || CB, "wide3, half2 and dma3t are cband geometries");
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
-                       : GEO == 3 ? kB2Half2Cb : GEO == 4 ? kB2Dma3Cb : GEO == 5 ? kB2Dma3tCb : kB2Wide;
+                       : GEO == 3 ? kB2Half2Cb : GEO == 4 ? (CB ? kB2Dma3Cb : kB2Dma3B2)
+                       : GEO == 5 ? kB2Dma3tCb : kB2Wide;
     // dma3: wave kLdWave stages the x windows (LDS-DMA, three buffers, two bands ahead) and
     // the other waves apply -- no x ever passes through an applying wave's registers, and
     // the loader's wait for its DMA is the only vmcnt wait on x (its queue holds nothing else).
@@ -230,9 +231,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t r0 = b * block_rows;
     const int32_t nr = min(block_rows, n_rows - r0);
     const __amdgpu_buffer_rsrc_t x_src = rsrc(x, (uint64_t)n_cols * 4);
-    constexpr uint32_t kBandBytes = CB ? 4u * 64u * (uint32_t)G.chunks() : 16384u;   // entries of one band
+    constexpr uint32_t kBandBytes = (CB ? 4u : 8u) * 64u * (uint32_t)G.chunks();   // entries of one band
     // Threads that hold entries (dma3: all but the loader wave, whose loads go past the range).
-    constexpr int kApplyThreads = CB ? 64 * G.chunks() / CPW : kB2Threads;
+    constexpr int kApplyThreads = 64 * G.chunks() / CPW;
     static_assert(kApplyThreads <= kB2Threads && kBandBytes % kApplyThreads == 0, "whole entry slots per lane");
     const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (int64_t)g0 * (kBandBytes / 4), (uint64_t)nb * kBandBytes);
     // Band windows: lane l holds clo of bands cw + l (lo) and cw + 64 + l (hi), read
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             // TPF (SM_LD_TPF=1, development A/B): band q+1's codebook values read during band q,
             // so after each barrier only the x and accumulator reads queue on the LDS -- measured
             // slower (35.5 vs 34.1 us: its wait for band q+1's entries, one band after their load).
-            constexpr bool kTpf = SM_LD_TPF != 0;
+            constexpr bool kTpf = SM_LD_TPF != 0 && CB;
             float tvn[CPW];
             if constexpr (kTpf) tab_read(E[0], tvn);
             for (int32_t p = 0; p < nbu; p += U) {
@@ -639,6 +640,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                     }
                     if constexpr (ABL & 1) {
                         asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
+                    } else if constexpr (!CB) {
+                        apply_b2(xs[u % 3], E[u % ER]);
                     } else if constexpr (kTpf) {
                         // band q's reads, then band q+1's codebook reads behind them (they
                         // land while band q adds), then band q's adds and writes
@@ -764,10 +767,10 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     const bool cb = xb.kind == kXbCband;
     const bool wide3 = cb && xb.band_cols == kB2Wide3Cb.window;
     const bool half2 = cb && xb.band_cols == kB2Half2Cb.window;
-    const bool dma3 = cb && xb.band_cols == kB2Dma3Cb.window;
+    const bool dma3 = xb.band_cols == kB2Dma3Cb.window;   // cband or band2 entries
     const bool dma3t = cb && xb.band_cols == kB2Dma3tCb.window;
     const bool tall = !wide3 && !half2 && !dma3 && !dma3t && xb.band_cols != kB2Wide.window;
-    const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? kB2Dma3Cb : dma3t ? kB2Dma3tCb
+    const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? (cb ? kB2Dma3Cb : kB2Dma3B2) : dma3t ? kB2Dma3tCb
                    : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
@@ -808,6 +811,11 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (dma3t) {
         if (abl != 0) return hipErrorInvalidValue;
         SM_B2(0, 2, true, 5);
+        return hipGetLastError();
+    }
+    if (dma3 && !cb) {
+        if (abl != 0) return hipErrorInvalidValue;
+        SM_B2(0, 2, false, 4);
         return hipGetLastError();
     }
     if (dma3 && abl != 2048) {
@@ -943,7 +951,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (half2) {
         SM_B2(0, 2, true, 3);
     } else if (dma3) {
-        SM_B2(0, 2, true, 4);
+        if (cb) SM_B2(0, 2, true, 4); else SM_B2(0, 2, false, 4);
     } else if (dma3t) {
         SM_B2(0, 2, true, 5);
     } else if (tall) {

@@ -138,6 +138,8 @@ constexpr B2Geom kB2Half2Cb{1 << 13, 15872, 14, 2, 14, 4};
 // 30 KiB buffers (7680 columns) and applies nothing; waves 0-14 apply chunks 2w, 2w+1 of
 // 30-chunk bands and never touch x in registers.  LDS: 3 x 30 KiB + 64 KiB + 4 table copies.
 constexpr B2Geom kB2Dma3Cb{1 << 14, 7680, 13, 2, 13, 4, 30};
+// dma3 for 8-byte band2 entries (word + fp32 value): the same loader and 30-chunk bands.
+constexpr B2Geom kB2Dma3B2{1 << 14, 7680, 13, 2, kCbColBits, 1, 30};
 // dma3 with 7168-column windows: 4 KiB freed for 8 table copies (development A/B).
 constexpr B2Geom kB2Dma3tCb{1 << 14, 7168, 13, 2, 13, 8, 30};
 

@@ -65,11 +65,11 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6])
 def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
-    """tall: 0 the default (cband: dma3), 1 tall, 6 wide (band2: the same as 0)."""
-    if tall == 6 and kind == "band2":
-        pytest.skip("band2's default is the wide geometry")
+    """tall: 0 the default (cband: dma3), 1 tall, 4 dma3 (band2's 8-byte entries in it), 6 wide."""
+    if (tall == 6 and kind == "band2") or (tall == 4 and kind == "cband"):
+        pytest.skip("the same geometry as tall = 0")
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
     M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind, tall)
     if slabs == 1:
@@ -128,7 +128,7 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6])
 def test_band2_special_values_and_signed_zeros(sm, kind, tall):
     n_rows, n_cols = 30000, 50000
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77,
@@ -156,7 +156,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6])
 def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
