@@ -331,10 +331,10 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                              int32_t geo_opt, int32_t slabs, bool forced) {
     const bool tall = geo_opt == 1;
     const bool half2 = geo_opt == 2 && kind == kXbCband;
-    // Codebook words default to dma3 (a loader wave stages x: config 2 34.0-34.6 vs 36.9-37.1
-    // us for the wide geometry); band_tall = 6 keeps the wide one.
-    const int32_t geo_req = geo_opt;
-    if (geo_opt == 0 && kind == kXbCband) geo_opt = 4;
+    // Both encodings default to dma3 (a loader wave stages x: config 2 34.0-34.6 vs 36.9-37.1
+    // us for the wide geometry with codebook words, 37.9-38.0 vs 38.6-38.7 with 8-byte
+    // entries); band_tall = 6 keeps the wide one.
+    if (geo_opt == 0) geo_opt = 4;   // dma3 for codebook words and 8-byte entries alike
     const bool dma3 = geo_opt == 4 || (geo_opt == 5 && kind == kXbCband);
     const B2Geom geom = half2 ? kB2Half2Cb : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
                       : !tall ? kB2Wide
@@ -356,7 +356,6 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
     if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5) {   // half2 / dma3: codebook words only
         if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb;
-        else if (geo_req == 0) g = kB2Wide;   // no codebook: 8-byte entries, wide geometry
         else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
         else return SM_OK;                    // a codebook-only geometry was asked for
     }

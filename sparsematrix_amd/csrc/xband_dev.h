@@ -23,7 +23,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 constexpr int kAuxNt = 2;   // non-temporal: entries are read once
 constexpr int kAuxSc1 = 16; // write-through store / L1-bypassing load (cross-CU hand-off)
 #ifndef SM_COMBINE_SKIP_OWN
-#define SM_COMBINE_SKIP_OWN 1   // the slab combine issues no load for the own slab's part
+#define SM_COMBINE_SKIP_OWN 0   // 1: no load for the own slab's part (A/B: no measurable gain)
 #endif
 
 // vmcnt retires in issue order: waiting until only the N most recent vector loads
