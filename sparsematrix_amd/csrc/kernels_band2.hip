@@ -87,6 +87,9 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_E_EARLY
 #define SM_E_EARLY 0
 #endif
+#ifndef SM_LD_XPF
+#define SM_LD_XPF 0
+#endif
 #ifndef SM_LD_TPF
 #define SM_LD_TPF 0
 #endif
@@ -157,7 +160,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     constexpr int kXBuf = kLd ? 3 : 2;   // x window buffers in LDS
     static_assert(!kDma || SM_CB_DMA_EAHEAD >= 4, "DMA variant: hipcc's entry waits must not stall");
     constexpr int AX = kDma ? 1 : CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
-    constexpr int AE = kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
+    // XPF (dma3 + codebook, SM_LD_XPF): band q+1's x and codebook values are read during band q,
+    // once the loader has flagged window q+1 in LDS, so after each barrier only the accumulator
+    // reads queue; its entries come 3 bands ahead (band q+1's must be in registers by then).
+    constexpr bool kXpf = kLd && CB && SM_LD_XPF != 0;
+    constexpr int AE = kXpf ? 3 : kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
     // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
     // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
     constexpr bool kEarly = SM_E_EARLY != 0;
@@ -183,6 +190,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // 38.6 with 4 on config 2; tall: one, no room for more).
     constexpr int kTabCopies = GEO == 0 ? SM_CB_TAB_COPIES : G.tab_copies;
     __shared__ float tab[CB ? 256 * kTabCopies : 1];
+    __shared__ int32_t s_xready;   // XPF: the highest window the loader has seen land
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     constexpr bool kProf = (ABL & 1024) != 0 && !kLd;
@@ -430,7 +438,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             tv[k] = tab[id * kTabCopies + (lane & (kTabCopies - 1))];
         }
     };
-    auto cb_read = [&](const float *xb, EV e, const float *tv_pre = nullptr) -> CbState {
+    auto cb_read = [&](const float *xb, EV e, const float *tv_pre = nullptr,
+                       const float *xv_pre = nullptr) -> CbState {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
         CbState st;
 #pragma unroll
@@ -442,7 +451,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             st.live[k] = __ballot(id != kCbDummyId);
             st.cont[k] = __ballot((int32_t)wd < 0);
             st.rl[k] = base + ((wd >> kCbOffSh) & kCbOffM);
-            st.xv[k] = xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd & kCbCol)];
+            st.xv[k] = xv_pre ? xv_pre[k] : xb[(ABL & 128) ? (uint32_t)(lane + 64 * k) : (wd & kCbCol)];
             st.tv[k] = (ABL & 32) ? __uint_as_float(id)
                        : tv_pre ? tv_pre[k] : tab[id * kTabCopies + (lane & (kTabCopies - 1))];
             st.yv[k] = yacc[st.rl[k]];
@@ -578,7 +587,11 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
     if constexpr (kLd) {
-        if (wid == kLdWave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wid == kLdWave) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (kXpf)
+                if (lane == 0) __hip_atomic_store(&s_xready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     } else if constexpr (!kDma) {
         store_x(0, X[0]);
     }
@@ -619,6 +632,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 } else {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
+                if constexpr (kXpf)   // window q+1 has landed: the appliers may read it now
+                    if (lane == 0) __hip_atomic_store(&s_xready, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if constexpr (kProfLd) mark_phase(4);
                 __syncthreads();
                 if constexpr (kProfLd) mark_phase(5);
@@ -627,9 +642,20 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             // TPF (SM_LD_TPF=1, development A/B): band q+1's codebook values read during band q,
             // so after each barrier only the x and accumulator reads queue on the LDS -- measured
             // slower (35.5 vs 34.1 us: its wait for band q+1's entries, one band after their load).
-            constexpr bool kTpf = SM_LD_TPF != 0 && CB;
+            constexpr bool kTpf = SM_LD_TPF != 0 && CB && !kXpf;
             float tvn[CPW];
             if constexpr (kTpf) tab_read(E[0], tvn);
+            float xpv[CPW], xpt[CPW];   // XPF: band q's x and codebook values, read during band q-1
+            auto xpf_read = [&](const float *xb, EV e) {
+#pragma unroll
+                for (int k = 0; k < CPW; ++k) {
+                    const uint32_t wd = e[k] ^ kCbDummy;
+                    const uint32_t id = (wd >> G.cb_col) & kCbDummyId;
+                    xpv[k] = xb[wd & kCbCol];
+                    xpt[k] = tab[id * kTabCopies + (lane & (kTabCopies - 1))];
+                }
+            };
+            if constexpr (kXpf) xpf_read(xs[0], E[0]);   // window 0 landed before the prologue barrier
             for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -642,6 +668,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                         asm volatile("" ::"v"(E[u % ER].x), "v"(E[u % ER].y));
                     } else if constexpr (!CB) {
                         apply_b2(xs[u % 3], E[u % ER]);
+                    } else if constexpr (kXpf) {
+                        CbState st = cb_read(xs[u % 3], E[u % ER], xpt, xpv);
+                        cb_finish(st);
+                        if (q + 1 < nb) {   // band q+1's window flagged, then its x and codebook reads
+                            while (__hip_atomic_load(&s_xready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q + 1)
+                                __builtin_amdgcn_s_sleep(1);
+                            xpf_read(xs[(u + 1) % 3], E[(u + 1) % ER]);
+                        }
                     } else if constexpr (kTpf) {
                         // band q's reads, then band q+1's codebook reads behind them (they
                         // land while band q adds), then band q's adds and writes
