@@ -870,7 +870,12 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
                     h[3] / wl / bands, h[4] / wl / bands, h[5] / wl / bands);
             break;
         }
-        case 0: SM_B2(0, 2, true, 4); break;
+        case 0:
+            if (prio == 1) SM_B2(0, 1, true, 4);
+            else if (prio == 3) SM_B2(0, 3, true, 4);
+            else if (prio == 0) SM_B2(0, 0, true, 4);
+            else SM_B2(0, 2, true, 4);
+            break;
         case 1: SM_B2(1, 2, true, 4); break;
         case 8: SM_B2(8, 2, true, 4); break;
         default: return hipErrorInvalidValue;
