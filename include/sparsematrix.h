@@ -220,7 +220,8 @@ typedef struct sm_build_opts {
     int32_t band_tall;         /* balanced bands: 1 = tall tiles (32K rows), 2 = half2
                                   tiles (8K rows, 15872-column windows; codebook only),
                                   4 = dma3 (a loader wave stages x by LDS-DMA into three
-                                  7680-column buffers; codebook only)                   */
+                                  7680-column buffers; the default), 6 = wide, 7 = dma3
+                                  tall (32K rows, 2560-column buffers; codebook only)   */
     int32_t gather_band_log2;  /* gather bands: 13, 14 or 15 (log2 columns), 0 = auto  */
     int32_t sell;              /* sorted sliced-ELL: -1 auto (built when no band layout), 0 never */
     int32_t sell_codebook;     /* sell slots as column|id words: -1 auto, 0 never      */

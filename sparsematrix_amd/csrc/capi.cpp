@@ -321,8 +321,9 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 // Builds into `d` the balanced bands of an n_rows x n_cols CSR (the matrix's own, or
 // the hot column prefix of a relabeled graph); `forced`: keep mostly-padding bands.
-// Geometry (sm_build_opts.band_tall): 0 = the default (dma3 for codebook words, wide
-// otherwise), 1 = tall, 2 = half2, 4 = dma3, 6 = wide; development
+// Geometry (sm_build_opts.band_tall): 0 = the default (dma3, both encodings), 1 = tall,
+// 2 = half2, 4 = dma3, 6 = wide, 7 = dma3 tall (codebook words; config 2: 41.5 vs 33.6 us,
+// DESIGN.md §3.4b); development
 // builds also take 3 = wide3 for codebook values (three chunks per wave, 12160-column
 // windows, one table copy; config 2: 38.5 vs 37.2 us wide -- the table's bank conflicts
 // cost what the third fewer bands save: 36.1 vs 36.2 us with the lookup ablated).
@@ -335,8 +336,10 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // us for the wide geometry with codebook words, 37.9-38.0 vs 38.6-38.7 with 8-byte
     // entries); band_tall = 6 keeps the wide one.
     if (geo_opt == 0) geo_opt = 4;   // dma3 for codebook words and 8-byte entries alike
-    const bool dma3 = geo_opt == 4 || (geo_opt == 5 && kind == kXbCband);
-    const B2Geom geom = half2 ? kB2Half2Cb : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
+    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7) && kind == kXbCband);
+    const B2Geom geom = half2 ? kB2Half2Cb
+                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb
+                                : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
                       : !tall ? kB2Wide
                       : kind == kXbCband ? kB2TallCb : kB2TallB2;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
@@ -354,8 +357,8 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     const bool wide3 = false;
 #endif
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
-    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5) {   // half2 / dma3: codebook words only
-        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : kB2Dma3tCb;
+    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7) {   // half2 / dma3*: codebook words
+        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : geo_opt == 5 ? kB2Dma3tCb : kB2Dma3TallCb;
         else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
         else return SM_OK;                    // a codebook-only geometry was asked for
     }
@@ -368,7 +371,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
     };
     bool ok = fits(g);
-    if (!ok && (g.cpw == 3 || g.chunks() == kB2Dma3Cb.chunks())) {   // wide3 / dma3 did not fit: wide
+    if (!ok && (g.cpw == 3 || g.nch != 0)) {   // wide3 / dma3* did not fit: wide
         g = kB2Wide;
         ok = fits(g);
     }

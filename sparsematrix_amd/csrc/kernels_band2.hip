@@ -126,14 +126,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
     int32_t *__restrict__ ctl, float alpha, float beta, int32_t xcd_map) {
     constexpr bool TALL = GEO == 1;
-    static_assert(GEO < 2 || GEO == 4 || CB, "wide3, half2 and dma3t are cband geometries");
+    static_assert(GEO < 2 || GEO == 4 || CB, "wide3, half2, dma3t and dma3 tall are cband geometries");
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
                        : GEO == 3 ? kB2Half2Cb : GEO == 4 ? (CB ? kB2Dma3Cb : kB2Dma3B2)
-                       : GEO == 5 ? kB2Dma3tCb : kB2Wide;
+                       : GEO == 5 ? kB2Dma3tCb : GEO == 6 ? kB2Dma3TallCb : kB2Wide;
     // dma3: wave kLdWave stages the x windows (LDS-DMA, three buffers, two bands ahead) and
     // the other waves apply -- no x ever passes through an applying wave's registers, and
     // the loader's wait for its DMA is the only vmcnt wait on x (its queue holds nothing else).
-    constexpr bool kLd = GEO == 4 || GEO == 5;
+    constexpr bool kLd = GEO == 4 || GEO == 5 || GEO == 6;
     constexpr int kLdWave = kB2Threads / 64 - 1;
     constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 if constexpr (kXpf)   // window q+1 has landed: the appliers may read it now
                     if (lane == 0) __hip_atomic_store(&s_xready, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if constexpr (kProfLd) mark_phase(4);
-                __syncthreads();
+                if constexpr (!(ABL & 512)) __syncthreads();   // 512: no band barriers (racy, A/B)
                 if constexpr (kProfLd) mark_phase(5);
             }
         } else {
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                         mark_phase(1);
                     }
                     E[u % ER] = load_e(q + AE);
-                    if (q < nb) __syncthreads();
+                    if (!(ABL & 512) && q < nb) __syncthreads();
                     if constexpr (kProfLd) mark_phase(2);
                 }
             }
@@ -803,9 +803,10 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     const bool half2 = cb && xb.band_cols == kB2Half2Cb.window;
     const bool dma3 = xb.band_cols == kB2Dma3Cb.window;   // cband or band2 entries
     const bool dma3t = cb && xb.band_cols == kB2Dma3tCb.window;
-    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && xb.band_cols != kB2Wide.window;
+    const bool dma3tall = cb && xb.band_cols == kB2Dma3TallCb.window;
+    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && !dma3tall && xb.band_cols != kB2Wide.window;
     const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? (cb ? kB2Dma3Cb : kB2Dma3B2) : dma3t ? kB2Dma3tCb
-                   : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+                   : dma3tall ? kB2Dma3TallCb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -847,6 +848,15 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         SM_B2(0, 2, true, 5);
         return hipGetLastError();
     }
+    if (dma3tall && abl != 2048) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true, 6); break;
+        case 1: SM_B2(1, 2, true, 6); break;
+        case 8: SM_B2(8, 2, true, 6); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (dma3 && !cb) {
         if (abl != 0) return hipErrorInvalidValue;
         SM_B2(0, 2, false, 4);
@@ -878,6 +888,8 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             break;
         case 1: SM_B2(1, 2, true, 4); break;
         case 8: SM_B2(8, 2, true, 4); break;
+        case 512: SM_B2(512, 2, true, 4); break;
+        case 520: SM_B2(520, 2, true, 4); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
@@ -941,6 +953,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             void *sym = nullptr;
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
             if (dma3) SM_B2(2048, 2, true, 4);
+            else if (dma3tall) SM_B2(2048, 2, true, 6);
             else SM_B2(2048, 2, true, 0);
             (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
             (void)hipStreamSynchronize(s);
@@ -993,6 +1006,8 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         if (cb) SM_B2(0, 2, true, 4); else SM_B2(0, 2, false, 4);
     } else if (dma3t) {
         SM_B2(0, 2, true, 5);
+    } else if (dma3tall) {
+        SM_B2(0, 2, true, 6);
     } else if (tall) {
         if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {

@@ -142,6 +142,12 @@ constexpr B2Geom kB2Dma3Cb{1 << 14, 7680, 13, 2, 13, 4, 30};
 constexpr B2Geom kB2Dma3B2{1 << 14, 7680, 13, 2, kCbColBits, 1, 30};
 // dma3 with 7168-column windows: 4 KiB freed for 8 table copies (development A/B).
 constexpr B2Geom kB2Dma3tCb{1 << 14, 7168, 13, 2, 13, 8, 30};
+// dma3 tall (cband only): 32K-row blocks (128 KiB of sums), three 2560-column buffers (30 KiB),
+// the table in one copy -- 159 KiB.  Half the x bytes per term of dma3: the band loop is bound
+// by the x windows' L2 -> LDS traffic, not by the apply.  20-chunk bands
+// (waves 0-9 apply, 10-14 idle at the barriers), 12-bit columns and 11-bit row offsets (a chunk's
+// rows span < 2048).
+constexpr B2Geom kB2Dma3TallCb{1 << 15, 2560, 13, 2, 12, 1, 20};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

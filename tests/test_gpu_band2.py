@@ -40,8 +40,15 @@ def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
                                  opts=dict(layout=kind, band_tall=tall, band_slabs=slabs or 0))
     info = M.info()
     assert info["has_xband"] == KINDS[kind], info
-    assert info["xband_block_rows"] <= (32768 if tall == 1 else 8192 if tall == 2 else 16384), info
+    assert info["xband_block_rows"] <= (32768 if tall in (1, 7) else 8192 if tall == 2 else 16384), info
     return M, info
+
+
+def _skip_geometry(kind, tall):
+    if (tall == 6 and kind == "band2") or (tall == 4 and kind == "cband"):
+        pytest.skip("the same geometry as tall = 0")
+    if tall == 7 and kind == "band2":
+        pytest.skip("dma3 tall is a codebook-word geometry")
 
 
 def _check(M, info, rp, ci, va, x, y0, alpha, beta, algo="xband"):
@@ -65,11 +72,11 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
 def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
-    """tall: 0 the default (cband: dma3), 1 tall, 4 dma3 (band2's 8-byte entries in it), 6 wide."""
-    if (tall == 6 and kind == "band2") or (tall == 4 and kind == "cband"):
-        pytest.skip("the same geometry as tall = 0")
+    """tall: 0 the default (cband: dma3), 1 tall, 4 dma3 (band2's 8-byte entries in it), 6 wide,
+    7 dma3 tall (codebook words only)."""
+    _skip_geometry(kind, tall)
     rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
     M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind, tall)
     if slabs == 1:
@@ -128,8 +135,9 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
 def test_band2_special_values_and_signed_zeros(sm, kind, tall):
+    _skip_geometry(kind, tall)
     n_rows, n_cols = 30000, 50000
     rp, ci, va = uniform_csr(n_rows, n_cols, 6, seed=77,
                              table=np.random.default_rng(1).uniform(-1, 1, 250).astype(np.float32))
@@ -156,10 +164,11 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
 def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
+    _skip_geometry(kind, tall)
     torch = torch_dev()
     n_rows, n_cols = 300000, 400000
     rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=21)
@@ -333,6 +342,31 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     torch.cuda.synchronize()
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
                            to_host(y0), 1.3, 0.5, 131072)
+    assert np.array_equal(bits(to_host(y)), bits(want))
+
+
+def test_cband_dma3_tall_config2_vs_slab_oracle(sm):
+    """Config 2 in the dma3 tall geometry (32K-row blocks, 8 slabs of 131072 columns, 20-chunk
+    bands of 2560 columns): bit-identical to the 8-slab restatement of the reference order."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=7))
+    info = M.info()
+    assert info["has_xband"] == 5 and info["xband_block_rows"] == 32768, info
+    assert info["xband_slabs"] == 8 and info["xband_slab_cols"] == 131072, info
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.3, 0.5)
+    M.spmv(x, y, 1.3, 0.5)   # a second launch: the epoch hand-off's next generation
+    torch.cuda.synchronize()
+    w1 = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
+                         to_host(y0), 1.3, 0.5, 131072)
+    want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
+                           w1, 1.3, 0.5, 131072)
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
