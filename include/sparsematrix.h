@@ -344,6 +344,14 @@ SM_API sm_status sm_panel_kernel(int32_t variant, int32_t m, int32_t n, int32_t 
 /* Synchronise the stream and report asynchronous kernel errors. */
 SM_API sm_status sm_stream_sync(sm_stream stream);
 
+/* Testing hook: set the slab hand-off launch counter of every row block of a band2 /
+ * cband layout (xband_dev.h, 64-bit, monotonic) to `started` and clear its arrival
+ * words, as if `started` tiles had run before -- e.g. 2^32 - 1 to run launches across
+ * the 32-bit boundary.  Synchronous; no SpMV on the matrix may be in flight.
+ * SM_ERR_NOT_SUPPORTED when the matrix has no multi-slab band2 / cband layout, or when
+ * `started` is not a whole number of launches (a multiple of the slab count). */
+SM_API sm_status sm_debug_seed_handoff(sm_matrix *m, uint64_t started);
+
 /* ---- multi-GPU: row partition + one RCCL all-gather per product ------------
  * SURVEY.md §8(e).  One process per GPU of one node.  Rank r holds its rows of B
  * (any contiguous split; sm_multi_partition gives the equal one) as an sm_matrix with
@@ -414,7 +422,11 @@ SM_API sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, const sm_matri
  * Buffer ordering: every product records, on the stream that ran it, that it has read
  * the gathered x; any later all-gather into that buffer waits for it, from whatever
  * stream.  Calls on one context therefore may come from several streams.  Inside a
- * stream capture, the captured products are ordered by the capture only. */
+ * stream capture, the captured products are ordered by the capture only: a graph replay
+ * is not tracked, so the caller orders replays of captured products against eager calls
+ * on other streams (an event after each replay).  A capture cannot grow the gather
+ * buffers (that needs a device sync): a captured product larger than every earlier one
+ * fails with SM_ERR_NOT_SUPPORTED -- run one eager product of that size first. */
 SM_API sm_status sm_multi_allgather(sm_multi *mc, const float *x_local, int32_t n_rhs,
                                     sm_stream stream, const float **x_full);
 /* Device timing of sm_multi_spmv / _spmm (HIP events around the all-gather and the

@@ -47,6 +47,7 @@ EXPORTS = (
     "sm_multi_last_error", "sm_multi_partition", "sm_multi_unique_id", "sm_multi_create",
     "sm_multi_destroy", "sm_multi_spmv", "sm_multi_spmm", "sm_multi_spmv_batch",
     "sm_multi_allgather", "sm_multi_set_timing", "sm_multi_last_times", "sm_multi_create_with",
+    "sm_debug_seed_handoff",
 )
 
 SM_UNIQUE_ID_BYTES = 128
@@ -157,6 +158,7 @@ def _declare(L):
         "sm_panel_kernel": ([_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _f32, _vp, _vp, _i32,
                              _vp, _i32, _vp], C.c_int),
         "sm_stream_sync": ([_vp], C.c_int),
+        "sm_debug_seed_handoff": ([_vp, C.c_uint64], C.c_int),
         "sm_multi_last_error": ([], C.c_char_p),
         "sm_multi_partition": ([_i64, _i32, _i32, C.POINTER(_i64), C.POINTER(_i64)], C.c_int),
         "sm_multi_unique_id": ([C.POINTER(SmUniqueId)], C.c_int),

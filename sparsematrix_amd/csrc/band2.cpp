@@ -380,7 +380,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
         geom.block_rows > ((int64_t)1 << (31 - kCbIdBits)))
         return false;
     const int64_t band_words = (int64_t)(ids ? 64 : 128) * geom.chunks();
-    if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
+    if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 30)) return false;   // x < 4 GiB: 32-bit buffer offsets
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)
             if (col[e] <= col[e - 1]) return false;

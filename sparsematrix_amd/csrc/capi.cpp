@@ -726,6 +726,7 @@ sm_status upload_exact_sell(sm_matrix *m, const int32_t *rp, const int32_t *col,
 // Column-swept row blocks (sweep.h, kernels_sweep.hip): forced by SM_LAYOUT_SWEEP.
 bool want_sweep(const sm_matrix *m) {
     if (m->nnz == 0 || m->n_rows == 0 || m->plan.xb.n_blocks > 0) return false;
+    if (m->n_cols >= ((int64_t)1 << 30)) return false;   // 32-bit byte offsets into x
     return m->opts.layout == SM_LAYOUT_SWEEP;
 }
 
@@ -1451,6 +1452,22 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
     return sm_get_info_ex(m, info, sizeof(sm_info));
 }
 
+sm_status sm_debug_seed_handoff(sm_matrix *m, uint64_t started) {
+    if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
+    const XbandDev &xb = m->plan.xb;
+    if (xb.n_blocks <= 0 || (xb.kind != kXbBand2 && xb.kind != kXbCband) || xb.n_slabs < 2 || !xb.d_tickets)
+        return fail(SM_ERR_NOT_SUPPORTED, "no multi-slab band2/cband layout");
+    if (started % (uint64_t)xb.n_slabs != 0)
+        return fail(SM_ERR_NOT_SUPPORTED, "started must be a multiple of the slab count");
+    DeviceGuard g(m->device);
+    // Control words per block (xband_dev.h slab_handoff_epoch): [0..1] started, [2..3] arrive.
+    std::vector<int32_t> h((size_t)xb.n_blocks * 4, 0);
+    for (int32_t b = 0; b < xb.n_blocks; ++b) memcpy(&h[(size_t)b * 4], &started, 8);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(xb.d_tickets, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    return e == hipSuccess ? SM_OK : hip_fail(e, "sm_debug_seed_handoff");
+}
+
 sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     if (!m || !out) return fail(SM_ERR_INVALID_ARG, "null argument");
     sm_info full;
@@ -1806,15 +1823,21 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         e = after_launch(e, s, "sm_addmatmat native");
         return e == hipSuccess ? SM_OK : hip_fail(e, "sm_addmatmat native");
     }
-    if (algo != SM_ALGO_PARITY && m <= (algo == SM_ALGO_EXACT ? 2 : 4) && n < ((int64_t)1 << 18) && k > 0) {
-        // A few right-hand sides on a matrix of few B rows: the row-panel kernel would give
-        // each B row one thread (n threads, a fraction of the chip), while the SpMV layouts
-        // spread a row's work -- and rows of A and C are contiguous (x = A row i, y = C row
-        // i), so m SpMVs need no transposes.  Same algo, so EXACT keeps the reference's
-        // order.  blas_test 16384^2 (row panel vs m SpMVs): AUTO m = 2 / 4 1.55 / 1.56 vs
-        // 0.48 / 0.96 ms; EXACT (its SpMV 0.45 ms) m = 2 1.55 vs 0.91, m = 4 1.56 vs 1.81.
+    // Few right-hand sides on a matrix of few B rows: the row-panel kernel gives each B row
+    // mp / 4 lanes, so at m <= 4 and n = 16384 it runs 16384 lanes, each a serial chain over
+    // its whole row.  Two remedies, both keeping every output's terms in stored order:
+    //  - short rows (<= 64 terms on average) and m <= 2: m SpMVs on A's and C's rows (x = A
+    //    row i, y = C row i, contiguous, no transposes), each with a reference-order kernel
+    //    (EXACT) so the result equals the row panel's bit for bit whatever m is;
+    //  - otherwise the row panel on a workspace padded to 16 columns (4 lanes per B row; the
+    //    padding columns are computed and never copied back).
+    // blas_test 16384^2 at 25 % (rows of ~4096 terms), AUTO, round 4: m = 4 0.957 ms as four
+    // SpMVs, m = 16 0.425 ms (profiles/r04_blas_test_16384_fewrhs.txt).
+    const bool few_rows = n < ((int64_t)1 << 18) && k > 0 && algo != SM_ALGO_PARITY;
+    if (few_rows && m <= 2 && mat->nnz <= 64 * n) {
+        const sm_algo sa = (algo == SM_ALGO_AUTO || algo == SM_ALGO_EXACT) ? SM_ALGO_EXACT : algo;
         for (int32_t i = 0; i < m; i++) {
-            const sm_status st = sm_spmv(mat, alpha, a + (int64_t)i * lda, beta, c + (int64_t)i * ldc, algo, stream);
+            const sm_status st = sm_spmv(mat, alpha, a + (int64_t)i * lda, beta, c + (int64_t)i * ldc, sa, stream);
             if (st != SM_OK) return st;
         }
         return SM_OK;
@@ -1834,7 +1857,7 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         // workspace, mp = m rounded up to 4 (the padding columns are never copied
         // back), then C = Y^T.  Same terms in the same order as the in-place kernel
         // below (bit-identical); the matrix is streamed once instead of m times.
-        const int64_t mp = (m + 3) & ~3;
+        const int64_t mp = few_rows && m < 16 ? 16 : (m + 3) & ~3;
         // The matrix's workspace (sm_internal.h), where the reference allocates a temp
         // buffer per call (sparse-matrix.cc:155-161): stream-ordered behind the previous
         // call's kernels, so back-to-back calls neither block the host nor share bytes.
@@ -1859,8 +1882,8 @@ sm_status sm_addmatmat(const sm_matrix *mat, const float *a, int32_t m, int32_t 
         queued = queued || e == hipSuccess;
         if (e == hipSuccess) e = launch_transpose(c, m, (int32_t)n, ldc, Y, mp, s);
         if (e == hipSuccess)
-            e = launch_spmm_rowpanel((int32_t)n, m, mat->d_row_ptr, mat->d_col, mat->d_val,
-                                     (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, true, s);
+            e = launch_spmm_rowpanel((int32_t)n, mp == 16 && m < 16 ? 16 : m, mat->d_row_ptr, mat->d_col,
+                                     mat->d_val, (int32_t)mat->nnz, X, mp, k, Y, mp, alpha, beta, true, s);
         if (e == hipSuccess) e = launch_transpose(Y, (int32_t)n, m, mp, c, ldc, s);
         if (queued) {   // recorded on the error path too: kernels may be queued
             const hipError_t er = hipEventRecord(mat->ws_ready, s);

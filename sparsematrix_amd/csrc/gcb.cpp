@@ -137,7 +137,9 @@ bool gcb_build(const int32_t *rp, const int32_t *col, const float *val, int64_t 
                int rows_log2, int32_t n_slabs, int32_t window, GcbHost &out) {
     out = GcbHost();
     if (rows_log2 < 6 || rows_log2 > 15 || window < 64 || window > kGcbMaxWindow) return false;
-    if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 31)) return false;
+    if (n_rows <= 0 || n_cols <= 0 || n_slabs < 1 || n_cols >= ((int64_t)1 << 30)) return false;
+    // x < 4 GiB: the kernel gathers x through one buffer resource with 32-bit byte offsets
+    // 4 * column; wider matrices fall back to the sliced ELL.
     for (int64_t r = 0; r < n_rows; r++)   // strictly ascending columns per row
         for (int32_t e = rp[r] + 1; e < rp[r + 1]; e++)
             if (col[e] <= col[e - 1]) return false;

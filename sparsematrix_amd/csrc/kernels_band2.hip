@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t b = t / n_slabs;
     const int32_t slab = t - b * n_slabs;
 #if SM_B2_EPOCH
-    const uint32_t old_started = (ABL & 8) ? 0u : handoff_begin(ctl + (int64_t)b * kCtlWords, n_slabs);
+    const uint64_t old_started = (ABL & 8) ? 0u : handoff_begin(ctl + (int64_t)b * kCtlWords, n_slabs);
 #else
     if (!(ABL & 8)) handoff_started(ctl + (int64_t)b * kCtlWords, n_slabs);
 #endif
@@ -599,7 +599,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
 #if SM_B2_EPOCH
     // The commit check's snapshot (xband_dev.h slab_handoff_epoch): read now, used after the
     // band loop, so its round trip hides behind the loop.
-    const uint32_t snap = (ABL & 8) ? 0u : handoff_snapshot(ctl + (int64_t)b * kCtlWords, n_slabs);
+    const uint64_t snap = (ABL & 8) ? 0u : handoff_snapshot(ctl + (int64_t)b * kCtlWords, n_slabs);
 #endif
 
     // Whole groups of U bands (static ring indices, no branch around a load or a

@@ -159,8 +159,17 @@ void release(sm_multi *mc) {
 // The gather buffers hold `floats` each, grown on demand: the new pair is allocated
 // first (on failure the old pair stays in place and the call fails), then the old pair
 // is released once the device is idle with respect to it.
-sm_status ensure_buffers(sm_multi *mc, size_t floats) {
+bool capturing(hipStream_t s);
+
+// Growing the gather buffers frees the old pair after a device-wide sync, which a stream
+// capture cannot contain (it would invalidate the capture): under capture the buffers must
+// already be large enough -- run one eager product of the largest n_rhs first.
+sm_status ensure_buffers(sm_multi *mc, size_t floats, hipStream_t s) {
     if (mc->xbuf_floats >= floats && mc->xbuf[0] && mc->xbuf[1]) return SM_OK;
+    if (s && capturing(s))
+        return mfail(SM_ERR_NOT_SUPPORTED, "gather buffers of %zu floats needed inside a stream capture "
+                     "(held: %zu): run one product of this size eagerly before capturing", floats,
+                     mc->xbuf_floats);
     float *nb[2] = {nullptr, nullptr};
     hipError_t e = hipSuccess;
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipMalloc((void **)&nb[i], floats * sizeof(float));
@@ -278,7 +287,7 @@ sm_status create_common(int32_t nranks, int32_t rank, const sm_matrix *local, sm
     if (e == hipSuccess) e = hipEventCreate(&mc->t1);
     if (e == hipSuccess) e = hipEventCreate(&mc->t2);
     sm_status st = e == hipSuccess ? SM_OK : hip_mfail(e, "sm_multi_create");
-    if (st == SM_OK) st = ensure_buffers(mc, (size_t)std::max<int64_t>(mc->n_cols, 1));
+    if (st == SM_OK) st = ensure_buffers(mc, (size_t)std::max<int64_t>(mc->n_cols, 1), nullptr);
     if (st != SM_OK) {
         release(mc);
         delete mc;
@@ -363,7 +372,7 @@ sm_status sm_multi_allgather(sm_multi *mc, const float *x_local, int32_t n_rhs, 
     std::lock_guard<std::mutex> lk(mc->mu);
     DevScope g(mc->device);
     hipStream_t s = (hipStream_t)stream;
-    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols * n_rhs);
+    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols * n_rhs, s);
     if (st == SM_OK) st = order_write(mc, 0, s);
     if (st == SM_OK) st = gather(mc, x_local, mc->xbuf[0], (size_t)mc->x_local_len * n_rhs, s);
     if (st == SM_OK) st = mark_read(mc, 0, s);   // later writers wait for the gather at least
@@ -379,7 +388,7 @@ namespace {
 sm_status one_product(sm_multi *mc, int32_t n_rhs, float alpha, const float *x_local, float beta,
                       float *y_local, int64_t ldy, sm_algo algo, hipStream_t s) {
     const size_t per = (size_t)std::max<int32_t>(n_rhs, 1);
-    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols * per);
+    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols * per, s);
     if (st == SM_OK) st = order_write(mc, 0, s);
     if (st != SM_OK) return st;
     hipError_t e = mc->timing ? hipEventRecord(mc->t0, s) : hipSuccess;
@@ -442,7 +451,7 @@ sm_status sm_multi_spmv_batch(sm_multi *mc, int32_t count, const sm_matrix *cons
     std::lock_guard<std::mutex> lk(mc->mu);
     DevScope g(mc->device);
     hipStream_t s = (hipStream_t)stream, c = mc->comm_stream;
-    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols);
+    sm_status st = ensure_buffers(mc, (size_t)mc->n_cols, s);
     if (st != SM_OK) return st;
     // The x slices were written on the caller's stream: the gathers start after them.
     hipError_t e = hipEventRecord(mc->start, s);

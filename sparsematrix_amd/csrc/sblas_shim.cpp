@@ -188,14 +188,16 @@ void SparseMatrix<P, V, T, brs, bcs>::AddMatMat(T *a, int32 m, int32 lda, T *c, 
     // result is the reference's bit for bit: m = 1 a reference-order SpMV layout (one
     // slab of bands, sliced ELL without segments, ...), m > 1 the row-panel SpMM.
     if (is_device_ptr(c)) {
-        // Device C: queued on the legacy default stream and not waited for -- every later
-        // null-stream operation (hipMemcpy, a kernel on the default stream) sees the
-        // result, which is what "C is updated on return" means for device memory.  The
-        // reference is synchronous only because it is CPU code.  A host A is uploaded.
+        // Device C: queued on the legacy default stream, then waited for, so C is final on
+        // return for every reader -- a non-blocking stream, a per-thread default stream, the
+        // host -- as the reference's synchronous call promises (sparse-matrix.cc:139-194),
+        // and an asynchronous kernel fault is reported here.
+        // A host A is uploaded.
         Staged<float> da(a, alpha != 0.0f ? span(m, lda, rows_) : 0);
         if (!da.ok) { fprintf(stderr, "AddMatMat: staging A failed\n"); return; }
-        report(sm_addmatmat(handle_, da.dev, m, lda, c, ldc, alpha, beta, SM_ALGO_EXACT, nullptr),
-               "AddMatMat");
+        const sm_status st = sm_addmatmat(handle_, da.dev, m, lda, c, ldc, alpha, beta, SM_ALGO_EXACT, nullptr);
+        report(st, "AddMatMat");
+        if (st == SM_OK) report(sm_stream_sync(nullptr), "AddMatMat");
     } else {
         report(sm_addmatmat_host(handle_, a, m, lda, c, ldc, alpha, beta), "AddMatMat");
     }

@@ -204,31 +204,34 @@ __device__ void slab_handoff(const float *yacc, int32_t *ctl, int32_t *s_word, f
 // words are never reset at the end of a launch, so no tile waits for a final "done" round
 // trip, and the commit check is a snapshot read early in the tile (its round trip hidden
 // behind the band loop) instead of a load at the start of the epilogue.
-//   [0] started  monotonic; each tile adds 1 at entry and keeps the old value: its
-//                launch's generation is g = old / S (launches on one matrix are ordered --
-//                stream order or the matrix's scratch event -- so every tile of a launch
-//                draws from [g S, g S + S));
-//   [1 + (g & 1)] arrive  for generation g as `arrive` above (count | commit bits); the
+//   [0..1] started  a 64-bit monotonic count; each tile adds 1 at entry and keeps the old
+//                value: its launch's generation is g = old / S (launches on one matrix are
+//                ordered -- stream order or the matrix's scratch event -- so every tile of a
+//                launch draws from [g S, g S + S)).  64 bits because g must be the same for
+//                every tile of a launch: a 32-bit count wraps after 2^32 / S launches, and
+//                where S does not divide 2^32 the launch across the wrap saw two different
+//                generations and hung.  2^64 / S launches of ~30 us are ~10^6 years.
+//   [2 + (g & 1)] arrive  for generation g as `arrive` above (count | commit bits); the
 //                slab-0 tile zeroes the other parity's word as it leaves -- its last user
 //                (launch g - 1) is complete, its next (launch g + 1) comes after this one.
 // A tile commits (waits for its siblings and combines its own part) when its snapshot of
 // started, read after the tile's prologue, shows all S tiles of generation g.
-__device__ __forceinline__ uint32_t handoff_begin(int32_t *ctl, int32_t n_slabs) {
+__device__ __forceinline__ uint64_t handoff_begin(int32_t *ctl, int32_t n_slabs) {
     if (n_slabs <= 1 || threadIdx.x != 0) return 0u;
-    return __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctl), 1u, __ATOMIC_RELAXED,
+    return __hip_atomic_fetch_add(reinterpret_cast<uint64_t *>(ctl), (uint64_t)1, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint32_t handoff_snapshot(const int32_t *ctl, int32_t n_slabs) {
+__device__ __forceinline__ uint64_t handoff_snapshot(const int32_t *ctl, int32_t n_slabs) {
     if (n_slabs <= 1) return 0u;
-    return __hip_atomic_load(reinterpret_cast<const uint32_t *>(ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int THREADS>
 __device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_word, float *y,
                                    float *partials, int32_t n_rows, int32_t r0, int32_t nr,
-                                   int32_t slab, int32_t n_slabs, bool y_vec, uint32_t old_started,
-                                   uint32_t snapshot) {
+                                   int32_t slab, int32_t n_slabs, bool y_vec, uint64_t old_started,
+                                   uint64_t snapshot) {
     const int32_t tid = threadIdx.x;
     const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
     float *outp = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * ps;
@@ -237,16 +240,16 @@ __device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_w
     const int32_t part = ((nr + n_slabs - 1) / n_slabs + 3) & ~3;
     auto part_lo = [&](int32_t s) { return min(s * part, nr); };
     auto part_hi = [&](int32_t s) { return min((s + 1) * part, nr); };
-    const uint32_t S = (uint32_t)n_slabs;
+    const uint64_t S = (uint64_t)n_slabs;
     if (tid == 0) {   // thread 0 holds the generation (handoff_begin)
-        const uint32_t g = old_started / S;
+        const uint64_t g = old_started / S;
         s_word[0] = n_slabs <= 16 && snapshot - g * S >= S;   // every sibling had started
-        s_word[3] = (int32_t)g;
+        s_word[3] = (int32_t)(g & 1u);
     }
     __syncthreads();
     const bool committed = s_word[0] != 0;
-    const uint32_t g = (uint32_t)s_word[3];
-    int32_t *arrive = ctl + 1 + (g & 1u);
+    const uint32_t g = (uint32_t)s_word[3];   // the generation's parity
+    int32_t *arrive = ctl + 2 + g;
     if (committed) {   // the own part stays in LDS
         publish_rows<THREADS>(yacc, outp, vec_out, 0, part_lo(slab), nr);
         publish_rows<THREADS>(yacc, outp, vec_out, part_hi(slab), nr, nr);
@@ -281,7 +284,7 @@ __device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_w
                                       part_lo(q), part_hi(q));
     }
     if (tid == 0 && slab == 0)   // the next launch's word (see above)
-        __hip_atomic_store(ctl + 1 + ((g + 1u) & 1u), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctl + 2 + (g ^ 1u), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace

@@ -276,6 +276,15 @@ int main() {
         std::vector<float> val = {1, 2, 3};
         bad += check_layout(rp, col, val, 1, 10, 1, false);
     }
+    {   // x of 4 GiB or more: 32-bit byte offsets into x would wrap, so the builder declines
+        const std::vector<int32_t> rp = {0, 2}, col = {3, (1 << 30) + 5};
+        const std::vector<float> val = {1.0f, 2.0f};
+        Band2Host h;
+        if (band2_build(rp.data(), col.data(), val.data(), 1, (int64_t)1 << 30, 1, h)) {
+            printf("band2_build accepted 2^30 columns\n");
+            bad++;
+        }
+    }
     printf(bad ? "band2_asan: FAILED\n" : "band2_asan: ok\n");
     return bad ? 1 : 0;
 }

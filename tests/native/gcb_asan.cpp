@@ -133,6 +133,22 @@ int main() {
         fails += check(rp, col, val, rows, cols, 14, 1, 1 << 18);
         fails += check(rp, col, val, rows, cols, 14, 2, 1 << 18);
     }
+    {   // x of 4 GiB or more: the kernel's 32-bit byte offsets into x would wrap, so the
+        // builder must decline -- here and in band2_build.
+        const std::vector<int32_t> rp = {0, 2}, col = {3, (1 << 30) + 5};
+        const std::vector<float> val = {1.0f, 2.0f};
+        GcbHost h;
+        for (int64_t cols : {(int64_t)1 << 30, ((int64_t)1 << 31) - 1})
+            if (gcb_build(rp.data(), col.data(), val.data(), 1, cols, 14, 1, 1 << 18, h)) {
+                printf("gcb_build accepted %lld columns (x >= 4 GiB)\n", (long long)cols);
+                fails++;
+            }
+        const std::vector<int32_t> col2 = {3, (1 << 30) - 5};
+        if (!gcb_build(rp.data(), col2.data(), val.data(), 1, ((int64_t)1 << 30) - 1, 14, 1, 1 << 18, h)) {
+            printf("gcb_build declined 2^30 - 1 columns\n");
+            fails++;
+        }
+    }
     if (fails) return 1;
     printf("gcb_asan: ok\n");
     return 0;

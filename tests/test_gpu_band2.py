@@ -188,6 +188,36 @@ def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     assert np.array_equal(first, bits(want))
 
 
+@pytest.mark.parametrize("kind", list(KINDS))
+@pytest.mark.parametrize("slabs", [3, 5])
+def test_handoff_counter_across_32bit_boundary(sm, kind, slabs):
+    """the epoch hand-off's launch counter.  A launch's generation is
+    g = started / S; with a 32-bit counter and S not dividing 2^32 the launch that crossed
+    the wrap gave its tiles different g and hung.  The counter is 64-bit now: seeded just
+    below 2^32 (a whole number of launches), four launches cross the boundary and every
+    product stays bit-identical to the slab-order oracle."""
+    import ctypes
+    torch = torch_dev()
+    n_rows, n_cols = 100000, 400000
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=31)
+    M, info = _band2(sm, rp, ci, va, n_cols, slabs, kind)
+    assert info["xband_slabs"] == slabs, info
+    seed = ((1 << 32) - 1) // slabs * slabs - slabs   # two launches below the 32-bit boundary
+    L = sm._lib.load()
+    assert L.sm_debug_seed_handoff(ctypes.c_void_p(M._require()), ctypes.c_uint64(seed)) == 0
+    assert L.sm_debug_seed_handoff(ctypes.c_void_p(M._require()), ctypes.c_uint64(seed + 1)) != 0
+    rng = np.random.default_rng(32)
+    x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    want = bits(slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"]))
+    ys = [to_dev(y0) for _ in range(4)]
+    for y in ys:
+        M.spmv(x, y, 1.0, 0.5)
+    torch.cuda.synchronize()
+    for y in ys:
+        assert np.array_equal(bits(to_host(y)), want)
+
+
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 def test_cband_half2_vs_oracle(sm, n_rows, n_cols, per_row):
     """The half2 geometry (8K-row blocks, 15872-column windows, 4 table copies):

@@ -730,6 +730,55 @@ def test_wide_matrix_dense_rows_fall_back_to_blocked(sm):
     assert_terms_close(to_host(y), want, absum)
 
 
+def test_addmatmat_few_rhs_on_harness_shape(sm):
+    """the reference harness's shape (blas_test 16384 x 16384, 25 %
+    density, rows of ~4096 terms) with few right-hand sides.  AUTO took 0.957 ms at m = 4
+    (four SpMVs) against 0.425 ms at m = 16; the row panel padded to 16 columns now serves
+    every m < 16 there.  AUTO's m = 4 must not be slower than its m = 16, and EXACT (the
+    reference's C++ surface) stays bit-identical to the reference order for m = 2, 4, 8."""
+    torch = torch_dev()
+    n_rows = n_cols = 16384
+    rng = np.random.default_rng(61)
+    rows = []
+    for r0 in range(0, n_rows, 2048):
+        mask = rng.random((2048, n_cols), dtype=np.float32) < 0.25
+        rows.append(mask)
+    mask = np.concatenate(rows)
+    ci = np.nonzero(mask)[1].astype(np.int32)
+    rp = np.zeros(n_rows + 1, np.int64)
+    rp[1:] = np.cumsum(mask.sum(axis=1))
+    del mask, rows
+    table = rng.uniform(-1, 1, 255).astype(np.float32)
+    va = table[rng.integers(0, 255, ci.size)]
+    M = sm.SparseMatrix.from_csr(rp.astype(np.int32), ci, va, n_cols)
+    k, n = M.NumRows(), M.NumCols()
+
+    def run(m, algo, reps):
+        A = rng.uniform(-1, 1, (m, k)).astype(np.float32)
+        C = rng.uniform(-1, 1, (m, n)).astype(np.float32)
+        a_d, c_d = to_dev(A.reshape(-1)), to_dev(C.reshape(-1))
+        M.AddMatMat(a_d, m, k, c_d, n, 1.3, 0.7, algo=algo)
+        torch.cuda.synchronize()
+        got = to_host(c_d).reshape(m, n)
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            M.AddMatMat(a_d, m, k, c_d, n, 1.3, 0.7, algo=algo)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return A, C, got, (sorted(ts)[len(ts) // 2] if ts else 0.0)
+
+    t = {m: run(m, "auto", 7)[3] for m in (4, 16)}
+    print("AUTO ms", t)
+    assert t[4] <= 1.1 * t[16] + 0.02, t
+    for m in (2, 4, 8):
+        A, C, got, _ = run(m, "exact", 0)
+        want = oracle.csr_spmm(rp, ci, va, np.ascontiguousarray(A.T), np.ascontiguousarray(C.T), 1.3, 0.7).T
+        assert bits_equal(got, np.ascontiguousarray(want)), m
+
+
 def test_addmatmat_workspace_back_to_back(sm):
     """Device AddMatMat (2 <= m <= 128) reuses the matrix's workspace: calls queued
     back to back on one stream (growing it in between) and calls on two streams at

@@ -10,7 +10,7 @@ cd "$ROOT" || exit 1
 STEPS=${STEPS:-all}
 run() { echo "== $*" ; "$@"; }
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  run timeout -k 10 900 python -m pytest tests -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 11; }
+  run timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 180 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 11; }
   tail -3 "$OUT/pytest_gpu.log"
 fi
 if [[ $STEPS == all || $STEPS == *smoke* ]]; then

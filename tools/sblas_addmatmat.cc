@@ -98,7 +98,14 @@ int main(int argc, char **argv) {
         HIP_OK(hipMemcpy(dC0, C0.data(), C0.size() * 4, hipMemcpyHostToDevice));
         HIP_OK(hipMemcpy(dC, dC0, C0.size() * 4, hipMemcpyDeviceToDevice));
         B.AddMatMat(dA, m, k, dC, n, alpha, beta);   // the checked result
-        HIP_OK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
+        {   // read C on a non-blocking stream, not ordered behind the null stream: the
+            // reference's AddMatMat is synchronous, so C must be final on return
+            hipStream_t rs;
+            HIP_OK(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
+            HIP_OK(hipMemcpyAsync(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost, rs));
+            HIP_OK(hipStreamSynchronize(rs));
+            HIP_OK(hipStreamDestroy(rs));
+        }
         auto timed = [&](auto &&call) {
             return median_ms(reps, [&] {
                 HIP_OK(hipMemcpy(dC, dC0, C0.size() * 4, hipMemcpyDeviceToDevice));
