@@ -204,8 +204,8 @@ def test_handoff_counter_across_32bit_boundary(sm, kind, slabs):
     assert info["xband_slabs"] == slabs, info
     seed = ((1 << 32) - 1) // slabs * slabs - slabs   # two launches below the 32-bit boundary
     L = sm._lib.load()
-    assert L.sm_debug_seed_handoff(ctypes.c_void_p(M._require()), ctypes.c_uint64(seed)) == 0
-    assert L.sm_debug_seed_handoff(ctypes.c_void_p(M._require()), ctypes.c_uint64(seed + 1)) != 0
+    assert L.sm_debug_seed_handoff(M._require(), ctypes.c_uint64(seed)) == 0
+    assert L.sm_debug_seed_handoff(M._require(), ctypes.c_uint64(seed + 1)) != 0
     rng = np.random.default_rng(32)
     x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)

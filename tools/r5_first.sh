@@ -9,3 +9,5 @@ cd "$ROOT" || exit 1
 timeout -k 10 180 ./build/xstream 50 > "$OUT/r5_xstream.txt" 2>&1 || { tail -20 "$OUT/r5_xstream.txt"; exit 21; }
 cat "$OUT/r5_xstream.txt"
 bash tools/gpu_check.sh
+timeout -k 10 400 python -u tools/rmat_gcb_ab.py 24 0 > "$OUT/r5_rmat_gcb_ab.txt" 2>&1 || { tail -20 "$OUT/r5_rmat_gcb_ab.txt"; exit 22; }
+cat "$OUT/r5_rmat_gcb_ab.txt"

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #define CK(x)                                                                       \
@@ -35,6 +36,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *base, uint64_
 }
 
 constexpr int kSlabBytes = 1 << 20;
+
+// One LDS read that hipcc cannot turn into a flat load (a volatile LDS pointer becomes a
+// flat_load, counted in vmcnt, and hipcc then drains vmcnt(0) before it).
+__device__ __forceinline__ uint32_t lds_touch(uint32_t addr) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
 constexpr int kLdsBytes = 150 * 1024;
 
 // One 1 KiB piece of x (byte offset voff per lane) into LDS at lds (wave-uniform).
@@ -70,7 +79,13 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
     const __amdgpu_buffer_rsrc_t e_src = rsrc(ent + (size_t)blockIdx.x * (kBandEnt / 4) * NB, (uint64_t)kBandEnt * NB);
     auto load_e = [&](int q) -> u32x2 {
         const uint32_t off = (E && wid < NAPPLY && q < NB) ? kBandEnt * (uint32_t)q + 8u * (uint32_t)tid : 0xFFFFFFF0u;
-        return __builtin_amdgcn_raw_buffer_load_b64(e_src, off, 0, 2);
+        u32x2 v;   // asm: hipcc tracks no load here, so it inserts no vmcnt drains of its own
+        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
+        return v;
+    };
+    // wait until only N younger vector-memory ops are pending, then use v
+    auto wait_use = [](u32x2 &v, auto n) {
+        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(v.x), "+v"(v.y) : "n"(decltype(n)::value) : "memory");
     };
     // issue the pieces of window q owned by this wave
     auto issue = [&](int q) {
@@ -90,41 +105,51 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
     // prologue: windows 0..A-1, entries 0..AE-1
     if (NLD == 0 || loader)
         for (int q = 0; q < A; ++q) issue(q);
+    if (!loader) {
 #pragma unroll
-    for (int v = 0; v < AE; ++v) ev[v] = load_e(v);
+        for (int v = 0; v < AE; ++v) ev[v] = load_e(v);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     constexpr int U = AE;   // unroll so the entry ring indices are static
-    for (int p = 0; p < NB; p += U) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = p + u;
-            if (q >= NB) break;
-            if (loader) {
+    if constexpr (NLD > 0) {
+        if (loader) {   // its own loop: no entry registers flow through it (hipcc would drain vmcnt)
+            for (int q = 0; q < NB; ++q) {
                 issue(q + A);   // into the buffer window q-1 left
                 // window q+1 landed: the younger (A-1) windows' pieces may fly
                 if constexpr (A == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL) : "memory");
                 else if constexpr (A == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPL) : "memory");
                 else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPL) : "memory");
-            } else if constexpr (NLD == 0) {
+                __syncthreads();
+            }
+        } else {
+            for (int p = 0; p < NB; p += U) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int q = p + u;
+                    wait_use(ev[u], std::integral_constant<int, AE - 1>());
+                    acc ^= ev[u].x ^ ev[u].y;
+                    ev[u] = load_e(q + AE);
+                    acc += lds_touch(lds0 + (uint32_t)((q % NBUF) * W + lane * 4));
+                    if (q < NB) __syncthreads();
+                }
+            }
+        }
+    } else {
+        for (int p = 0; p < NB; p += U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = p + u;
                 // window q and entries q landed: the ops younger than the younger of the two
                 // may fly (issue order per band r: window r+A's pieces, then entries r+AE)
                 constexpr int X = AE <= A ? (AE - 1) * (PPL + 1) : 1 + (A - 1) * (PPL + 1);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
-                __syncthreads();   // every wave's pieces of window q
+                wait_use(ev[u], std::integral_constant<int, X>());
+                if (q < NB) __syncthreads();   // every wave's pieces of window q
                 acc ^= ev[u].x ^ ev[u].y;
-                acc += *(volatile uint32_t *)&lds[(q % NBUF) * W + (lane * 4)];
+                acc += lds_touch(lds0 + (uint32_t)((q % NBUF) * W + lane * 4));
                 issue(q + A);      // into the buffer window q-1 left (every wave is past it)
                 ev[u] = load_e(q + AE);
-                continue;
-            } else {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AE - 1) : "memory");
-                acc ^= ev[u].x ^ ev[u].y;
-                ev[u] = load_e(q + AE);
             }
-            // touch the window (one LDS read) so the loop is not empty
-            acc += *(volatile uint32_t *)&lds[(q % NBUF) * W + (lane * 4)];
-            __syncthreads();
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -178,7 +203,6 @@ int main(int argc, char **argv) {
     run<1, 45, 2, 2, true>(x, ent, out, reps);
     run<2, 45, 2, 2, true>(x, ent, out, reps);
     run<4, 45, 2, 2, true>(x, ent, out, reps);
-    run<1, 48, 2, 2, false>(x, ent, out, reps);
     run<2, 48, 2, 2, true>(x, ent, out, reps);
     run<1, 16, 4, 2, true>(x, ent, out, reps);
     run<2, 16, 4, 2, true>(x, ent, out, reps);
