@@ -83,7 +83,7 @@ def main():
     print(f"terms per 32K-row tile: max {int(tile_terms.max())} mean {float(tile_terms.float().mean()):.0f} "
           f"(max/mean {float(tile_terms.max()) / float(tile_terms.float().mean()):.1f}); the longest tile is one "
           f"CU's serial work", flush=True)
-    variants = [(s, False) for s in slab_list] + [(slab_list[0], True)]
+    variants = [(s, False) for s in slab_list] + ([] if os.environ.get("RMAT_GCB_NO_SHUFFLE") else [(slab_list[0], True)])
     for slabs, shuffle in variants:
         rpv, civ, vav = rp, ci2, va2
         if shuffle:   # rows in random order: every tile gets ~ the mean (y gathered / scattered per SpMV)

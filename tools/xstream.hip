@@ -156,6 +156,49 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
     if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
+// Pure streaming, no barrier: NLD waves each keep K 1 KiB LDS-DMA pieces in flight
+// (s_waitcnt vmcnt(K) after every issue) until the tile's 1 MiB slab is in LDS (written
+// round-robin over a 64 KiB region; the data is not used).  Per-CU L2 -> LDS rate against
+// the number of pieces in flight.
+template <int NLD, int K>
+__global__ __launch_bounds__(1024) void xflow_kernel(const float *__restrict__ x, uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int slab = blockIdx.x & 3;
+    const __amdgpu_buffer_rsrc_t x_src = rsrc(x + (size_t)slab * (kSlabBytes / 4), kSlabBytes);
+    const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t *)&lds[0];
+    if (wid < NLD) {
+        constexpr int P = kSlabBytes / 1024 / NLD;   // pieces per loader
+        for (int k = 0; k < P; ++k) {
+            const int m = wid + k * NLD;
+            dma_piece(x_src, (uint32_t)(m * 1024 + lane * 16),
+                      __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((m & 63) * 1024)));
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0 && lds_touch(lds0) == 0x12345678u) out[blockIdx.x] = 1;
+}
+
+template <int NLD, int K>
+void run_flow(const float *x, uint32_t *out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((xflow_kernel<NLD, K>), dim3(256), dim3(1024), 0, 0, x, out);
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((xflow_kernel<NLD, K>), dim3(256), dim3(1024), 0, 0, x, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const float us = 1000.f * ms / reps;
+    printf("flow: %2d loader waves x %2d pieces in flight (%4d KiB per CU): %7.2f us/launch  %6.1f GB/s per CU\n",
+           NLD, K, NLD * K, us, (double)kSlabBytes / (us * 1e3));
+}
+
 template <int NLD, int WK, int A, int AE, bool E>
 float run(const float *x, const uint32_t *ent, uint32_t *out, int reps) {
     hipEvent_t a, b;
@@ -190,6 +233,27 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&ent, ent_bytes));
     CK(hipMemset(ent, 0, ent_bytes));
     CK(hipMalloc(&out, 4096));
+    if (argc > 2 && argv[2][0] == 'f') {   // streaming ceiling only
+        run_flow<1, 8>(x, out, reps);
+        run_flow<1, 16>(x, out, reps);
+        run_flow<1, 32>(x, out, reps);
+        run_flow<1, 56>(x, out, reps);
+        run_flow<2, 16>(x, out, reps);
+        run_flow<2, 32>(x, out, reps);
+        run_flow<2, 56>(x, out, reps);
+        run_flow<4, 8>(x, out, reps);
+        run_flow<4, 16>(x, out, reps);
+        run_flow<4, 32>(x, out, reps);
+        run_flow<4, 56>(x, out, reps);
+        run_flow<8, 8>(x, out, reps);
+        run_flow<8, 16>(x, out, reps);
+        run_flow<8, 32>(x, out, reps);
+        run_flow<16, 4>(x, out, reps);
+        run_flow<16, 8>(x, out, reps);
+        run_flow<16, 16>(x, out, reps);
+        run_flow<16, 32>(x, out, reps);
+        return 0;
+    }
     // dma3 as built: 1 loader, 30 KiB windows, 3 buffers
     run<1, 30, 2, 2, true>(x, ent, out, reps);
     run<1, 30, 2, 2, false>(x, ent, out, reps);
@@ -209,6 +273,10 @@ int main(int argc, char **argv) {
     run<4, 16, 4, 2, true>(x, ent, out, reps);
     run<2, 36, 3, 2, true>(x, ent, out, reps);
     run<4, 36, 3, 2, true>(x, ent, out, reps);
+    run<4, 30, 3, 2, true>(x, ent, out, reps);   // 4 buffers of 30 KiB: more in flight (120 KiB, not available)
+    run<2, 23, 3, 2, true>(x, ent, out, reps);   // 4 buffers of 23 KiB = 92 KiB (what fits beside the sums)
+    run<4, 23, 3, 2, true>(x, ent, out, reps);
+    run<3, 30, 2, 2, true>(x, ent, out, reps);
     run<0, 48, 2, 2, true>(x, ent, out, reps);
     run<0, 36, 3, 2, true>(x, ent, out, reps);
     return 0;
