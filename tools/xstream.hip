@@ -117,7 +117,8 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
             for (int q = 0; q < NB; ++q) {
                 issue(q + A);   // into the buffer window q-1 left
                 // window q+1 landed: the younger (A-1) windows' pieces may fly
-                if constexpr (A == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL) : "memory");
+                if constexpr (A == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else if constexpr (A == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL) : "memory");
                 else if constexpr (A == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPL) : "memory");
                 else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPL) : "memory");
                 __syncthreads();
@@ -233,6 +234,20 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&ent, ent_bytes));
     CK(hipMemset(ent, 0, ent_bytes));
     CK(hipMalloc(&out, 4096));
+    if (argc > 2 && argv[2][0] == 'a') {   // two buffers (window q+1 issued at band q)
+        run<1, 46, 1, 2, true>(x, ent, out, reps);
+        run<2, 46, 1, 2, true>(x, ent, out, reps);
+        run<4, 46, 1, 2, true>(x, ent, out, reps);
+        run<8, 46, 1, 2, true>(x, ent, out, reps);
+        run<4, 46, 1, 2, false>(x, ent, out, reps);
+        run<4, 40, 1, 2, true>(x, ent, out, reps);
+        run<4, 32, 1, 2, true>(x, ent, out, reps);
+        run<8, 32, 1, 2, true>(x, ent, out, reps);
+        run<4, 30, 2, 2, true>(x, ent, out, reps);
+        run<8, 30, 2, 2, true>(x, ent, out, reps);
+        run<1, 30, 2, 2, true>(x, ent, out, reps);
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'f') {   // streaming ceiling only
         run_flow<1, 8>(x, out, reps);
         run_flow<1, 16>(x, out, reps);
