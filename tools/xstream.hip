@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t lds_touch(uint32_t addr) {
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
     return v;
 }
-constexpr int kLdsBytes = 150 * 1024;
+constexpr int kLdsBytes = 160 * 1024;
 
 // One 1 KiB piece of x (byte offset voff per lane) into LDS at lds (wave-uniform).
 __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t src, uint32_t voff, uint32_t lds) {
@@ -57,7 +57,7 @@ __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t src, uint32_t v
         : "memory");
 }
 
-template <int NLD, int WK, int A, int AE, bool E>
+template <int NLD, int WK, int A, int AE, bool E, int CS = 0>
 __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__ x,
                                                        const uint32_t *__restrict__ ent,
                                                        uint32_t *__restrict__ out) {
@@ -132,6 +132,22 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
                     acc ^= ev[u].x ^ ev[u].y;
                     ev[u] = load_e(q + AE);
                     acc += lds_touch(lds0 + (uint32_t)((q % NBUF) * W + lane * 4));
+                    if constexpr (CS > 0) {   // the apply's LDS traffic: per chunk x, table, sum reads, sum write
+                        constexpr uint32_t kAcc = NBUF * W, kTab = kAcc + 65536;
+                        static_assert(kTab + 4096 <= kLdsBytes, "LDS");
+#pragma unroll
+                        for (int k = 0; k < CS; ++k) {
+                            const uint32_t h = (uint32_t)lane * 2654435761u ^ (uint32_t)q * 40503u ^ (uint32_t)(wid * CS + k) * 2246822519u;
+                            const uint32_t ax = lds0 + (uint32_t)((q % NBUF) * W) + ((h >> 7) % (uint32_t)(W / 4)) * 4u;
+                            const uint32_t aa = lds0 + kAcc + ((h >> 3) & 16383u) * 4u;
+                            const uint32_t at = lds0 + kTab + ((h >> 20) & 255u) * 16u + (lane & 3) * 4u;
+                            uint32_t vx, va, vt;
+                            asm volatile("ds_read_b32 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)\n\t"
+                                         "v_add_u32 %1, %1, %0\n\tv_add_u32 %1, %1, %2\n\tds_write_b32 %4, %1"
+                                         : "=&v"(vx), "=&v"(va), "=&v"(vt) : "v"(ax), "v"(aa), "v"(at) : "memory");
+                            acc += va;
+                        }
+                    }
                     if (q < NB) __syncthreads();
                 }
             }
@@ -200,7 +216,7 @@ void run_flow(const float *x, uint32_t *out, int reps) {
            NLD, K, NLD * K, us, (double)kSlabBytes / (us * 1e3));
 }
 
-template <int NLD, int WK, int A, int AE, bool E>
+template <int NLD, int WK, int A, int AE, bool E, int CS = 0>
 float run(const float *x, const uint32_t *ent, uint32_t *out, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -209,18 +225,18 @@ float run(const float *x, const uint32_t *ent, uint32_t *out, int reps) {
     // with x), so entries come from HBM as in the bench
     constexpr size_t kCopy = (size_t)32 << 20;   // uint32 words = 128 MiB
     for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
+        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
     CK(hipEventRecord(a));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
+        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     const float us = 1000.f * ms / reps;
     constexpr int NB = (kSlabBytes + WK * 1024 - 1) / (WK * 1024);
-    printf("NLD %d  W %3d KiB  A %d  AE %d  entries %d  bands %3d : %7.2f us/launch  x %6.1f GB/s per CU  %5.3f us/band\n",
-           NLD, WK, A, AE, (int)E, NB, us, (double)NB * WK * 1024 / (us * 1e3), us / NB);
+    printf("NLD %d  W %3d KiB  A %d  AE %d  entries %d  apply-sim %d chunks  bands %3d : %7.2f us/launch  x %6.1f GB/s per CU  %5.3f us/band\n",
+           NLD, WK, A, AE, (int)E, CS, NB, us, (double)NB * WK * 1024 / (us * 1e3), us / NB);
     return us;
 }
 
@@ -234,6 +250,21 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&ent, ent_bytes));
     CK(hipMemset(ent, 0, ent_bytes));
     CK(hipMalloc(&out, 4096));
+    if (argc > 2 && argv[2][0] == 'b') {   // two buffers, entries further ahead, simulated apply
+        run<1, 30, 2, 2, true, 2>(x, ent, out, reps);    // dma3 with its apply's LDS traffic
+        run<2, 40, 1, 4, true>(x, ent, out, reps);
+        run<2, 40, 1, 4, false>(x, ent, out, reps);
+        run<4, 45, 1, 4, true>(x, ent, out, reps);
+        run<4, 45, 1, 6, true>(x, ent, out, reps);
+        run<8, 45, 1, 4, true>(x, ent, out, reps);
+        run<2, 40, 1, 4, true, 3>(x, ent, out, reps);    // 14 appliers x 3 chunks
+        run<4, 45, 1, 4, true, 4>(x, ent, out, reps);    // 12 appliers x 4 chunks
+        run<4, 40, 1, 4, true, 4>(x, ent, out, reps);
+        run<8, 45, 1, 4, true, 6>(x, ent, out, reps);    // 8 appliers x 6 chunks
+        run<2, 30, 2, 4, true, 2>(x, ent, out, reps);
+        run<4, 30, 2, 4, true, 3>(x, ent, out, reps);
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'a') {   // two buffers (window q+1 issued at band q)
         run<1, 46, 1, 2, true>(x, ent, out, reps);
         run<2, 46, 1, 2, true>(x, ent, out, reps);
