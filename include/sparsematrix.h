@@ -142,6 +142,9 @@ typedef struct sm_info {
                                    0: not built) that SM_ALGO_EXACT runs                   */
     int32_t exact_algo;         /* the sm_algo SM_ALGO_EXACT runs for a 16-byte aligned x
                                    (SM_ALGO_SELL also for the unsegmented sliced ELL)       */
+    int32_t xband_slab0_cols;   /* columns of slab 0 (slab s >= 1 covers [slab0 + (s-1) *
+                                   xband_slab_cols, slab0 + s * xband_slab_cols)); equal to
+                                   xband_slab_cols when the slabs are even                  */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -241,6 +244,11 @@ typedef struct sm_build_opts {
                                   SM_ALGO_EXACT when no built layout keeps the reference's order
                                   for every row: 0 auto (matrices from the dense index, i.e.
                                   the reference's CopyForm path), 1 always, -1 never        */
+    int32_t band_slab0_permille; /* balanced bands with several slabs: slab 0's columns as a
+                                  share of an even split, in permille (0 = auto: 930).  The
+                                  slab-0 tile also loads and scales y before its first band, so
+                                  it gets fewer columns and every slab's tile ends together;
+                                  the other slabs share the rest evenly.  1000 = even slabs  */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);

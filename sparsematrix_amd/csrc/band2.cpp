@@ -370,7 +370,8 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
 }  // namespace
 
 bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
-                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids, B2Geom geom) {
+                 int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids, B2Geom geom,
+                 int32_t slab0_permille) {
     out = Band2Host();
     out.codebook = ids != nullptr;
     out.geom = geom;
@@ -386,9 +387,21 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
             if (col[e] <= col[e - 1]) return false;
     const int32_t br = (int32_t)std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
-    // Slabs of whole 256-column pieces.
-    const int64_t sc = ((n_cols + n_slabs - 1) / n_slabs + 255) & ~(int64_t)255;
-    const int64_t ns = (n_cols + sc - 1) / sc;
+    // Slabs of whole 256-column pieces; slab 0 may be narrower (slab0_permille of an even
+    // share), the others split the rest evenly.
+    int64_t sc = ((n_cols + n_slabs - 1) / n_slabs + 255) & ~(int64_t)255;
+    int64_t ns = (n_cols + sc - 1) / sc;
+    int64_t s0 = sc;
+    if (ns > 1 && slab0_permille > 0 && slab0_permille < 1000) {
+        s0 = std::max<int64_t>(256, (sc * slab0_permille / 1000 + 255) & ~(int64_t)255);
+        if (s0 < sc) {
+            sc = ((n_cols - s0 + ns - 2) / (ns - 1) + 255) & ~(int64_t)255;
+            ns = 1 + (n_cols - s0 + sc - 1) / sc;
+        } else {
+            s0 = sc;
+        }
+    }
+    auto slab_lo = [&](int64_t s) { return s == 0 ? (int64_t)0 : std::min<int64_t>(n_cols, s0 + (s - 1) * sc); };
     const int64_t ntile = nblk * ns;
     if (ntile >= ((int64_t)1 << 30)) return false;
     std::vector<TileOut> tiles((size_t)ntile);
@@ -398,8 +411,8 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
         th.emplace_back([&, t] {
             for (int64_t i = t; i < ntile; i += nthr) {
                 const int64_t b = i / ns, s = i % ns;
-                build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), s * sc,
-                           std::min<int64_t>(n_cols, (s + 1) * sc), geom, tiles[(size_t)i]);
+                build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), slab_lo(s),
+                           slab_lo(s + 1), geom, tiles[(size_t)i]);
             }
         });
     for (auto &x : th) x.join();
@@ -407,6 +420,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out.n_blocks = (int32_t)nblk;
     out.n_slabs = (int32_t)ns;
     out.slab_cols = (int32_t)sc;
+    out.slab0_cols = (int32_t)s0;
     out.tile_band_start.resize((size_t)ntile + 1);
     int64_t nb = 0;
     for (int64_t i = 0; i < ntile; i++) {

@@ -185,6 +185,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.ccsell_chunk_log2 = d.ccsell_chunk_log2;
         r.hot_cols = d.hot_cols;
         r.exact_sell = d.exact_sell;
+        r.band_slab0_permille = d.band_slab0_permille;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -196,6 +197,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     }
     if (const char *e = dev_env("SM_BAND_TALL")) r.band_tall = atoi(e);
     if (const char *e = dev_env("SM_BAND2_SLABS")) r.band_slabs = atoi(e);
+    if (const char *e = dev_env("SM_BAND_SLAB0")) r.band_slab0_permille = atoi(e);
     if (const char *e = dev_env("SM_XBAND_GBAND")) r.gather_band_log2 = atoi(e);
     if (const char *e = dev_env("SM_RELABEL")) r.relabel = atoi(e);
     if (const char *e = dev_env("SM_SELL")) r.sell = atoi(e) ? -1 : 0;
@@ -230,6 +232,8 @@ sm_status check_opts(const sm_build_opts *o) {
         return fail(SM_ERR_INVALID_ARG, "ccsell_chunk_log2 must be 0 or 8..24");
     if (r.hot_cols < -1) return fail(SM_ERR_INVALID_ARG, "hot_cols must be -1, 0 or positive");
     if (r.exact_sell < -1 || r.exact_sell > 1) return fail(SM_ERR_INVALID_ARG, "exact_sell must be -1, 0 or 1");
+    if (r.band_slab0_permille != 0 && (r.band_slab0_permille < 500 || r.band_slab0_permille > 1000))
+        return fail(SM_ERR_INVALID_ARG, "band_slab0_permille must be 0 or 500..1000");
     return SM_OK;
 }
 
@@ -329,7 +333,7 @@ bool want_xband(const sm_matrix *m) {
 // cost what the third fewer bands save: 36.1 vs 36.2 us with the lookup ablated).
 static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
-                             int32_t geo_opt, int32_t slabs, bool forced) {
+                             int32_t geo_opt, int32_t slabs, bool forced, int32_t slab0_permille = 1000) {
     const bool tall = geo_opt == 1;
     const bool half2 = geo_opt == 2 && kind == kXbCband;
     // Both encodings default to dma3 (a loader wave stages x: config 2 34.0-34.6 vs 36.9-37.1
@@ -366,7 +370,8 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
     // bytes than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
     auto fits = [&](const B2Geom &gg) {
-        if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, gg)) return false;
+        if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, gg, slab0_permille))
+            return false;
         return forced || bh.n_bands == 0 ||
                (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
     };
@@ -410,6 +415,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_bands = (int32_t)std::min<int64_t>(bh.n_bands, INT32_MAX);
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
+    d.slab0_cols = bh.slab0_cols;
     d.n_chunks = bh.n_bands * g.chunks();
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
@@ -419,8 +425,13 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
     // Geometry: band_tall (xband.h B2Geom, build_band2).
+    // Slab 0's tile loads and scales y (64 KiB per 16K-row block from HBM) before its first
+    // band: on config 2 its band loop ended 1.5-2.3 us after the other slabs' (per-tile
+    // timeline, profiles/r05_dma3_tile_timeline_dump.txt), and every block's hand-off waits
+    // for it -- so slab 0 gets 930 permille of an even share of the columns.
+    const int32_t p0 = m->opts.band_slab0_permille > 0 ? m->opts.band_slab0_permille : kB2Slab0Permille;
     return build_band2(m, m->plan.xb, m->n_rows, m->n_cols, m->nnz, rp, col, val, kind,
-                       m->opts.band_tall, m->opts.band_slabs, kind_forced(m));
+                       m->opts.band_tall, m->opts.band_slabs, kind_forced(m), p0);
 }
 
 // Gathered chunk bands (gcb.h, kernels_gcb.hip): 32K-row tiles where the rows make at
@@ -1496,6 +1507,7 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
         : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb
             ? m->plan.xb.slab_bands   // band2 / cband / gcb keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
+    info->xband_slab0_cols = m->plan.xb.slab0_cols > 0 ? m->plan.xb.slab0_cols : info->xband_slab_cols;
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;

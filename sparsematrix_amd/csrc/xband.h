@@ -153,6 +153,7 @@ struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)
     B2Geom geom = kB2Wide;
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
+    int32_t slab0_cols = 0;              // slab 0 = [0, slab0_cols), slab s >= 1 = [slab0 + (s-1) slab_cols, ...)
     int32_t max_bands_per_tile = 0;
     int64_t n_bands = 0;                 // over all tiles
     std::vector<int32_t> tile_band_start;   // n_blocks * n_slabs + 1 (tile t = b * S + s)
@@ -164,9 +165,11 @@ struct Band2Host {
 // Returns false when the layout does not apply: unsorted columns or size limits
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
 // ids != nullptr builds the cband encoding: ids[e] = codebook id (< 255) of term e.
+// slab0_permille: slab 0's columns as a share of an even split (1000 = even slabs).
+constexpr int32_t kB2Slab0Permille = 930;
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
-                 B2Geom geom = kB2Wide);
+                 B2Geom geom = kB2Wide, int32_t slab0_permille = 1000);
 
 // Codebook of a value array: table[ids[e]] has the bits of val[e] for every e; false
 // when there are more than 255 distinct bit patterns (table then undefined).

@@ -89,21 +89,26 @@ def with_env(key: str, value: str, fn):
             os.environ[key] = old
 
 
-def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int):
-    """The multi-slab band layouts' sum, restated on the oracle: each column slab
-    [s*slab_cols, (s+1)*slab_cols) summed in the reference's order (oracle.csr_spmv)
-    -- slab 0 from beta*y, later slabs from -0.0 -- then the slab sums added in slab
-    order in fp32.  Bit-exact target for has_xband 2/3/4 with several slabs."""
+def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int, slab0_cols: int | None = None):
+    """The multi-slab band layouts' sum, restated on the oracle: each column slab summed in
+    the reference's order (oracle.csr_spmv) -- slab 0 from beta*y, later slabs from -0.0 --
+    then the slab sums added in slab order in fp32.  Slab 0 covers [0, slab0_cols), slab
+    s >= 1 [slab0_cols + (s-1) slab_cols, slab0_cols + s slab_cols) (sm_info.xband_slab0_cols
+    / xband_slab_cols; even slabs when slab0_cols is None).  Bit-exact target for has_xband
+    2/3/4/5/6 with several slabs."""
     import oracle
     rp = np.asarray(rp, np.int64)
     ci = np.asarray(ci)
     va = np.asarray(va, np.float32)
     n = rp.size - 1
     n_cols = x.size
-    n_slabs = max(1, -(-n_cols // slab_cols))
+    s0 = slab_cols if slab0_cols is None else slab0_cols
+    n_slabs = 1 + max(0, -(-(n_cols - s0) // slab_cols))
     out = None
     for s in range(n_slabs):
-        mask = (ci >= s * slab_cols) & (ci < (s + 1) * slab_cols)
+        lo = 0 if s == 0 else s0 + (s - 1) * slab_cols
+        hi = s0 + s * slab_cols
+        mask = (ci >= lo) & (ci < hi)
         cm = np.concatenate([[0], np.cumsum(mask)])
         rps = np.zeros(n + 1, np.int64)
         rps[1:] = cm[rp[1:]] - cm[rp[:-1]]

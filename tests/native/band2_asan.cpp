@@ -17,9 +17,9 @@ using namespace smamd;
 
 static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
                         const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
-                        bool expect_ok, B2Geom geom = kB2Wide) {
+                        bool expect_ok, B2Geom geom = kB2Wide, int permille = 1000) {
     Band2Host h;
-    const bool ok = band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, nullptr, geom);
+    const bool ok = band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, nullptr, geom, permille);
     const uint32_t kDummy = geom.dummy_word();
     const int kCol = geom.col_bits;
     if (ok != expect_ok) { printf("FAIL build=%d expected %d\n", ok, expect_ok); return 1; }
@@ -30,7 +30,9 @@ static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_
     int64_t terms = 0;
     for (int64_t t = 0; t < (int64_t)h.n_blocks * h.n_slabs; t++) {
         const int64_t b = t / h.n_slabs, s = t % h.n_slabs;
-        const int64_t c0 = s * h.slab_cols, c1 = std::min<int64_t>(n_cols, c0 + h.slab_cols);
+        // slab 0 = [0, slab0_cols), slab s >= 1 = [slab0 + (s-1) slab_cols, + slab_cols)
+        const int64_t c0 = s == 0 ? 0 : h.slab0_cols + (s - 1) * (int64_t)h.slab_cols;
+        const int64_t c1 = std::min<int64_t>(n_cols, s == 0 ? h.slab0_cols : c0 + h.slab_cols);
         int64_t prev_hi = c0;
         for (int64_t g = h.tile_band_start[t]; g < h.tile_band_start[t + 1]; g++) {
             const int64_t clo = h.band_clo[g];
@@ -94,14 +96,14 @@ static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_
 // the chunk's 2048-row span, ids decode to the term's exact value bits.
 static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
                            const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
-                           B2Geom geom = kB2Wide) {
+                           B2Geom geom = kB2Wide, int permille = 1000) {
     std::vector<float> table;
     std::vector<uint8_t> ids;
     if (!codebook_ids(val.data(), (int64_t)val.size(), table, ids)) { printf("FAIL codebook\n"); return 1; }
     for (size_t e = 0; e < val.size(); e++)
         if (memcmp(&table[ids[e]], &val[e], 4) != 0) { printf("FAIL codebook id\n"); return 1; }
     Band2Host h;
-    if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data(), geom)) {
+    if (!band2_build(rp.data(), col.data(), val.data(), n_rows, n_cols, slabs, h, ids.data(), geom, permille)) {
         printf("FAIL cband build\n"); return 1; }
     const int cpw = geom.cpw, nch = geom.chunks();
     const size_t bw = (size_t)64 * nch;
@@ -113,7 +115,9 @@ static int check_layout_cb(const std::vector<int32_t> &rp, const std::vector<int
     int64_t terms = 0;
     for (int64_t t = 0; t < (int64_t)h.n_blocks * h.n_slabs; t++) {
         const int64_t b = t / h.n_slabs, s = t % h.n_slabs;
-        const int64_t c0 = s * h.slab_cols, c1 = std::min<int64_t>(n_cols, c0 + h.slab_cols);
+        // slab 0 = [0, slab0_cols), slab s >= 1 = [slab0 + (s-1) slab_cols, + slab_cols)
+        const int64_t c0 = s == 0 ? 0 : h.slab0_cols + (s - 1) * (int64_t)h.slab_cols;
+        const int64_t c1 = std::min<int64_t>(n_cols, s == 0 ? h.slab0_cols : c0 + h.slab_cols);
         for (int64_t g = h.tile_band_start[t]; g < h.tile_band_start[t + 1]; g++) {
             const int64_t clo = h.band_clo[g];
             for (int c = 0; c < nch; c++) {
@@ -184,6 +188,8 @@ static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned se
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2TallCb);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Wide3Cb);
+        // the AUTO geometry (dma3) with slab 0 narrower, as sm_create_* builds it
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Dma3Cb, kB2Slab0Permille);
     }
     return bad;
 }

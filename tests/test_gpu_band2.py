@@ -58,7 +58,7 @@ def _check(M, info, rp, ci, va, x, y0, alpha, beta, algo="xband"):
     if info["xband_slabs"] == 1:
         want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     else:
-        want = slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"])
+        want = slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(got), bits(want)), (alpha, beta, info["xband_slabs"])
     ref = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
@@ -159,7 +159,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
             M.spmv(to_dev(x), y, alpha, beta, algo="xband")
             got = to_host(y)
             want = (oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta) if info["xband_slabs"] == 1
-                    else slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"]))
+                    else slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"]))
             assert np.array_equal(bits(got), bits(want))
 
 
@@ -184,7 +184,7 @@ def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     first = bits(to_host(ys[0]))
     for y in ys[1:]:
         assert np.array_equal(bits(to_host(y)), first)
-    want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"])
+    want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(first, bits(want))
 
 
@@ -209,7 +209,7 @@ def test_handoff_counter_across_32bit_boundary(sm, kind, slabs):
     rng = np.random.default_rng(32)
     x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
-    want = bits(slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"]))
+    want = bits(slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"]))
     ys = [to_dev(y0) for _ in range(4)]
     for y in ys:
         M.spmv(x, y, 1.0, 0.5)
@@ -249,7 +249,7 @@ def test_cband_half2_config2_vs_slab_oracle(sm):
     y = y0.clone()
     M.spmv(x, y, 1.0, 0.5)
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
-                           1.0, 0.5, info["xband_slab_cols"])
+                           1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
@@ -288,7 +288,7 @@ def test_cband_dma3_special_values_and_repeats(sm):
     x[-1] = np.inf                     # the last column, inside the last window
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     y0[:300] = -0.0
-    want = slab_order_spmv(rp, ci, va, x, y0, 1.0, 0.5, info["xband_slab_cols"])
+    want = slab_order_spmv(rp, ci, va, x, y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     xd = to_dev(x)
     ys = [to_dev(y0) for _ in range(6)]
     for y in ys:
@@ -313,25 +313,26 @@ def test_cband_dma3_config2_vs_slab_oracle(sm):
     y = y0.clone()
     M.spmv(x, y, 1.0, 0.5)
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
-                           1.0, 0.5, info["xband_slab_cols"])
+                           1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
 def test_band2_config2_equals_blocked(sm):
-    """BASELINE config 2 (2^20 x 2^20, 16 terms/row): cband (AUTO), band2 and the
-    blocked kind use the same 4 slabs of 262144 columns and sum each in the
-    reference's order, so their results are bit-identical."""
+    """BASELINE config 2 (2^20 x 2^20, 16 terms/row): cband, band2 and the blocked kind
+    built on the same 4 even slabs of 262144 columns (band_slab0_permille = 1000; AUTO makes
+    slab 0 narrower) sum each in the reference's order, so their results are bit-identical."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
-    Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n)
-    Mb2 = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="band2"))
+    Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(band_slab0_permille=1000))
+    Mb2 = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="band2", band_slab0_permille=1000))
     Mbl = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="blocked"))
     ic, i2, ib = Mcb.info(), Mb2.info(), Mbl.info()
     assert ic["has_xband"] == 5 and i2["has_xband"] == 4 and ib["has_xband"] == 2
     assert ic["xband_slabs"] == i2["xband_slabs"] == ib["xband_slabs"] == 4
     assert ic["xband_slab_cols"] == i2["xband_slab_cols"] == ib["xband_slab_cols"] == 262144
+    assert ic["xband_slab0_cols"] == i2["xband_slab0_cols"] == ib["xband_slab0_cols"] == 262144
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -363,7 +364,7 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout=kind, band_tall=1))
     info = M.info()
     assert info["has_xband"] == KINDS[kind] and info["xband_block_rows"] == 32768, info
-    assert info["xband_slabs"] == 8 and info["xband_slab_cols"] == 131072, info
+    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] < info["xband_slab_cols"], info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -371,7 +372,7 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     M.spmv(x, y, 1.3, 0.5)
     torch.cuda.synchronize()
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
-                           to_host(y0), 1.3, 0.5, 131072)
+                           to_host(y0), 1.3, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
@@ -385,7 +386,7 @@ def test_cband_dma3_tall_config2_vs_slab_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=7))
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_block_rows"] == 32768, info
-    assert info["xband_slabs"] == 8 and info["xband_slab_cols"] == 131072, info
+    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] < info["xband_slab_cols"], info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -394,9 +395,9 @@ def test_cband_dma3_tall_config2_vs_slab_oracle(sm):
     M.spmv(x, y, 1.3, 0.5)   # a second launch: the epoch hand-off's next generation
     torch.cuda.synchronize()
     w1 = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
-                         to_host(y0), 1.3, 0.5, 131072)
+                         to_host(y0), 1.3, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x),
-                           w1, 1.3, 0.5, 131072)
+                           w1, 1.3, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
@@ -412,7 +413,8 @@ def test_config2_auto_full_size_vs_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n)
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_slabs"] == 4, info
-    assert info["xband_slab_cols"] == 262144, info
+    # slab 0 narrower (kB2Slab0Permille), the other three share the rest
+    assert info["xband_slab0_cols"] == 243968 and info["xband_slab_cols"] == 268288, info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -421,7 +423,7 @@ def test_config2_auto_full_size_vs_oracle(sm):
     got = to_host(y)
     rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
     xh, y0h = to_host(x), to_host(y0)
-    want = slab_order_spmv(rph, cih, vah, xh, y0h, 1.0, 0.5, 262144)
+    want = slab_order_spmv(rph, cih, vah, xh, y0h, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(got), bits(want))
     ref = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.0, 0.5, threads=16)
     _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.0, 0.5)
@@ -475,7 +477,7 @@ def test_concurrent_spmvs_on_two_streams(sm):
     rng = np.random.default_rng(32)
     xs = [to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32)) for _ in range(8)]
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
-    want = [slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"])
+    want = [slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
             for x in xs]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     ys = [to_dev(y0) for _ in xs]

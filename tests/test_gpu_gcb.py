@@ -38,7 +38,7 @@ def _check(M, info, rp, ci, va, x, y0, alpha, beta, algo="xband"):
     if info["xband_slabs"] == 1:
         want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     else:
-        want = slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"])
+        want = slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(bits(got), bits(want)), (alpha, beta, info["xband_slabs"])
     ref = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
@@ -115,7 +115,7 @@ def test_gcb_ragged_special_values(sm):
         M.spmv(to_dev(x), y, 1.3, 0.0)
         got = to_host(y)
         want = (oracle.csr_spmv(rp, ci, va, x, y0, 1.3, 0.0) if info["xband_slabs"] == 1
-                else slab_order_spmv(rp, ci, va, x, y0, 1.3, 0.0, info["xband_slab_cols"]))
+                else slab_order_spmv(rp, ci, va, x, y0, 1.3, 0.0, info["xband_slab_cols"], info["xband_slab0_cols"]))
         assert np.array_equal(bits(got), bits(want)), info["xband_slabs"]
 
 
@@ -129,6 +129,6 @@ def test_gcb_repeated_launches_reset_handoff(sm):
     ys = [to_dev(y0) for _ in range(6)]
     for y in ys:
         M.spmv(x, y, 1.0, 0.5)
-    want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"])
+    want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     for y in ys:
         assert np.array_equal(bits(to_host(y)), bits(want))

@@ -57,7 +57,7 @@ __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t src, uint32_t v
         : "memory");
 }
 
-template <int NLD, int WK, int A, int AE, bool E, int CS = 0>
+template <int NLD, int WK, int A, int AE, bool E, int CS = 0, int EP = 2>
 __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__ x,
                                                        const uint32_t *__restrict__ ent,
                                                        uint32_t *__restrict__ out) {
@@ -80,7 +80,14 @@ __global__ __launch_bounds__(1024) void xstream_kernel(const float *__restrict__
     auto load_e = [&](int q) -> u32x2 {
         const uint32_t off = (E && wid < NAPPLY && q < NB) ? kBandEnt * (uint32_t)q + 8u * (uint32_t)tid : 0xFFFFFFF0u;
         u32x2 v;   // asm: hipcc tracks no load here, so it inserts no vmcnt drains of its own
-        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
+        if constexpr (EP == 2)
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
+        else if constexpr (EP == 1)
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen sc0" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
+        else if constexpr (EP == 3)
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen sc0 sc1" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
+        else
+            asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(e_src) : "memory");
         return v;
     };
     // wait until only N younger vector-memory ops are pending, then use v
@@ -216,7 +223,7 @@ void run_flow(const float *x, uint32_t *out, int reps) {
            NLD, K, NLD * K, us, (double)kSlabBytes / (us * 1e3));
 }
 
-template <int NLD, int WK, int A, int AE, bool E, int CS = 0>
+template <int NLD, int WK, int A, int AE, bool E, int CS = 0, int EP = 2>
 float run(const float *x, const uint32_t *ent, uint32_t *out, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -225,18 +232,18 @@ float run(const float *x, const uint32_t *ent, uint32_t *out, int reps) {
     // with x), so entries come from HBM as in the bench
     constexpr size_t kCopy = (size_t)32 << 20;   // uint32 words = 128 MiB
     for (int i = 0; i < 3; ++i)
-        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
+        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS, EP>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
     CK(hipEventRecord(a));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
+        hipLaunchKernelGGL((xstream_kernel<NLD, WK, A, AE, E, CS, EP>), dim3(256), dim3(1024), 0, 0, x, ent + (i & 3) * kCopy, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     const float us = 1000.f * ms / reps;
     constexpr int NB = (kSlabBytes + WK * 1024 - 1) / (WK * 1024);
-    printf("NLD %d  W %3d KiB  A %d  AE %d  entries %d  apply-sim %d chunks  bands %3d : %7.2f us/launch  x %6.1f GB/s per CU  %5.3f us/band\n",
-           NLD, WK, A, AE, (int)E, CS, NB, us, (double)NB * WK * 1024 / (us * 1e3), us / NB);
+    printf("NLD %d  W %3d KiB  A %d  AE %d  entries %d (policy %d)  apply-sim %d chunks  bands %3d : %7.2f us/launch  x %6.1f GB/s per CU  %5.3f us/band\n",
+           NLD, WK, A, AE, (int)E, EP, CS, NB, us, (double)NB * WK * 1024 / (us * 1e3), us / NB);
     return us;
 }
 
@@ -250,6 +257,17 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&ent, ent_bytes));
     CK(hipMemset(ent, 0, ent_bytes));
     CK(hipMalloc(&out, 4096));
+    if (argc > 2 && argv[2][0] == 'c') {   // entry cache policy: 0 default, 1 sc0, 2 nt, 3 sc0 sc1
+        run<4, 45, 1, 4, true, 0, 0>(x, ent, out, reps);
+        run<4, 45, 1, 4, true, 0, 1>(x, ent, out, reps);
+        run<4, 45, 1, 4, true, 0, 2>(x, ent, out, reps);
+        run<4, 45, 1, 4, true, 0, 3>(x, ent, out, reps);
+        run<1, 30, 2, 2, true, 0, 0>(x, ent, out, reps);
+        run<1, 30, 2, 2, true, 0, 2>(x, ent, out, reps);
+        run<8, 45, 1, 4, true, 0, 0>(x, ent, out, reps);
+        run<8, 45, 1, 4, true, 6, 0>(x, ent, out, reps);
+        return 0;
+    }
     if (argc > 2 && argv[2][0] == 'b') {   // two buffers, entries further ahead, simulated apply
         run<1, 30, 2, 2, true, 2>(x, ent, out, reps);    // dma3 with its apply's LDS traffic
         run<2, 40, 1, 4, true>(x, ent, out, reps);
