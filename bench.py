@@ -192,7 +192,7 @@ def main():
     ap.add_argument("--layout", default="auto",
                     help="A/B: force the matrix layout (sm_build_opts.layout name, e.g. gcb, gather)")
     ap.add_argument("--band-tall", type=int, default=0,
-                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2, 4 dma3, 6 wide, 7 dma3 tall) for the config-2 matrices")
+                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2, 4 dma3, 6 wide, 7 dma3 tall, 8 dmaw) for the config-2 matrices")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")

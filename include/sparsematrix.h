@@ -245,10 +245,9 @@ typedef struct sm_build_opts {
                                   for every row: 0 auto (matrices from the dense index, i.e.
                                   the reference's CopyForm path), 1 always, -1 never        */
     int32_t band_slab0_permille; /* balanced bands with several slabs: slab 0's columns as a
-                                  share of an even split, in permille (0 = auto: 930).  The
-                                  slab-0 tile also loads and scales y before its first band, so
-                                  it gets fewer columns and every slab's tile ends together;
-                                  the other slabs share the rest evenly.  1000 = even slabs  */
+                                  share of an even split, in permille (0 = auto = 1000, even
+                                  slabs); the other slabs share the rest evenly.  The slab-0
+                                  tile also loads and scales y before its first band        */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);

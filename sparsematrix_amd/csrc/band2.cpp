@@ -375,7 +375,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out = Band2Host();
     out.codebook = ids != nullptr;
     out.geom = geom;
-    if ((!ids && geom.cpw != 2) || geom.cpw < 1 || geom.cpw > 4 ||
+    if ((!ids && geom.cpw != 2) || geom.cpw < 1 || geom.cpw > 8 ||
         geom.window > (1 << geom.col_bits) || (ids && geom.window > (1 << geom.cb_col)) ||
         geom.block_rows > ((int64_t)1 << (32 - geom.col_bits - kB2RankBits)) ||
         geom.block_rows > ((int64_t)1 << (31 - kCbIdBits)))

@@ -340,9 +340,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // us for the wide geometry with codebook words, 37.9-38.0 vs 38.6-38.7 with 8-byte
     // entries); band_tall = 6 keeps the wide one.
     if (geo_opt == 0) geo_opt = 4;   // dma3 for codebook words and 8-byte entries alike
-    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7) && kind == kXbCband);
+    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7 || geo_opt == 8) && kind == kXbCband);
     const B2Geom geom = half2 ? kB2Half2Cb
-                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb
+                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb : geo_opt == 8 ? kB2DmawCb
                                 : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
                       : !tall ? kB2Wide
                       : kind == kXbCband ? kB2TallCb : kB2TallB2;
@@ -361,8 +361,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     const bool wide3 = false;
 #endif
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
-    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7) {   // half2 / dma3*: codebook words
-        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : geo_opt == 5 ? kB2Dma3tCb : kB2Dma3TallCb;
+    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7 || geo_opt == 8) {   // half2 / dma3* / dmaw: codebook words
+        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : geo_opt == 5 ? kB2Dma3tCb
+                    : geo_opt == 8 ? kB2DmawCb : kB2Dma3TallCb;
         else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
         else return SM_OK;                    // a codebook-only geometry was asked for
     }
@@ -427,8 +428,8 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     // Geometry: band_tall (xband.h B2Geom, build_band2).
     // Slab 0's tile loads and scales y (64 KiB per 16K-row block from HBM) before its first
     // band: on config 2 its band loop ended 1.5-2.3 us after the other slabs' (per-tile
-    // timeline, profiles/r05_dma3_tile_timeline_dump.txt), and every block's hand-off waits
-    // for it -- so slab 0 gets 930 permille of an even share of the columns.
+    // timeline, profiles/r05_dma3_tile_timeline_dump.txt).  Narrower slab-0 tiles did not
+    // shorten the kernel (kB2Slab0Permille), so AUTO keeps even slabs; the option stays.
     const int32_t p0 = m->opts.band_slab0_permille > 0 ? m->opts.band_slab0_permille : kB2Slab0Permille;
     return build_band2(m, m->plan.xb, m->n_rows, m->n_cols, m->nnz, rp, col, val, kind,
                        m->opts.band_tall, m->opts.band_slabs, kind_forced(m), p0);

@@ -62,6 +62,10 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #ifndef SM_CB_EAHEAD
 #define SM_CB_EAHEAD 2
 #endif
+// dmaw: entries this many bands ahead (two-buffer windows leave no band of slack for them).
+#ifndef SM_CBW_EAHEAD
+#define SM_CBW_EAHEAD 4
+#endif
 #ifndef SM_B2_XAHEAD
 #define SM_B2_XAHEAD 2
 #endif
@@ -107,6 +111,7 @@ __device__ unsigned long long g_b2_ts[3 * 4096];
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
 // ABL (development only, SM_BAND2_ABLATE; results wrong): 1 skips the apply,
 // 2 the x loads and stores, 4 the entry loads, 8 the slab hand-off (plain stores),
@@ -129,12 +134,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     static_assert(GEO < 2 || GEO == 4 || CB, "wide3, half2, dma3t and dma3 tall are cband geometries");
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
                        : GEO == 3 ? kB2Half2Cb : GEO == 4 ? (CB ? kB2Dma3Cb : kB2Dma3B2)
-                       : GEO == 5 ? kB2Dma3tCb : GEO == 6 ? kB2Dma3TallCb : kB2Wide;
+                       : GEO == 5 ? kB2Dma3tCb : GEO == 6 ? kB2Dma3TallCb : GEO == 8 ? kB2DmawCb : kB2Wide;
+    static_assert(GEO != 8 || CB, "dmaw is a codebook geometry");
     // dma3: wave kLdWave stages the x windows (LDS-DMA, three buffers, two bands ahead) and
     // the other waves apply -- no x ever passes through an applying wave's registers, and
     // the loader's wait for its DMA is the only vmcnt wait on x (its queue holds nothing else).
-    constexpr bool kLd = GEO == 4 || GEO == 5 || GEO == 6;
-    constexpr int kLdWave = kB2Threads / 64 - 1;
+    constexpr bool kLd = GEO == 4 || GEO == 5 || GEO == 6 || GEO == 8;
+    constexpr bool kW = GEO == 8;                         // dmaw: 8 loader waves, two x buffers
+    constexpr int kNLd = kW ? 8 : 1;                      // loader waves (the last ones)
+    constexpr int kLdWave = kB2Threads / 64 - kNLd;       // the first loader wave
     constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
     constexpr int W = G.window;
@@ -157,14 +165,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // only the AE-1 younger entry loads -- at least the 3 ops really pending then
     // (one entry load, the window's two DMA pieces) once AE >= 4: no extra stall.
     constexpr bool kDma = CB && GEO == 0 && SM_CB_DMA != 0;
-    constexpr int kXBuf = kLd ? 3 : 2;   // x window buffers in LDS
+    constexpr int kXBuf = kLd && !kW ? 3 : 2;   // x window buffers in LDS
     static_assert(!kDma || SM_CB_DMA_EAHEAD >= 4, "DMA variant: hipcc's entry waits must not stall");
     constexpr int AX = kDma ? 1 : CB ? SM_CB_XAHEAD : SM_B2_XAHEAD;
     // XPF (dma3 + codebook, SM_LD_XPF): band q+1's x and codebook values are read during band q,
     // once the loader has flagged window q+1 in LDS, so after each barrier only the accumulator
     // reads queue; its entries come 3 bands ahead (band q+1's must be in registers by then).
     constexpr bool kXpf = kLd && CB && SM_LD_XPF != 0;
-    constexpr int AE = kXpf ? 3 : kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
+    constexpr int AE = kW ? SM_CBW_EAHEAD : kXpf ? 3 : kDma ? SM_CB_DMA_EAHEAD : CB ? SM_CB_EAHEAD : SM_B2_EAHEAD;
     // SM_E_EARLY (development A/B): the entries of band p+AE are loaded before band p's
     // apply into a ring of AE+1 slots (the slot of band p-1 is free by then).
     constexpr bool kEarly = SM_E_EARLY != 0;
@@ -175,8 +183,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     constexpr int ER = kEarly ? AE + 1 : AE;   // entry ring slots
     constexpr int U0 = AX > ER ? AX : ER;
     constexpr int UA = U0 % 2 ? 2 * U0 : (U0 % AX ? U0 * AX : U0);   // loop unroll: static roles
-    constexpr int U = kLd ? (ER % 3 == 0 ? 2 * ER : 6 * ER / (ER % 2 ? 1 : 2)) : UA;
-    static_assert(U % AX == 0 && U % ER == 0 && U % 2 == 0 && (!kLd || U % 3 == 0), "ring sizes divide the unroll");
+    constexpr int U = kW ? (ER % 2 ? 2 * ER : ER) : kLd ? (ER % 3 == 0 ? 2 * ER : 6 * ER / (ER % 2 ? 1 : 2)) : UA;
+    static_assert(U % AX == 0 && U % ER == 0 && U % 2 == 0 && (!kLd || U % kXBuf == 0), "ring sizes divide the unroll");
     static_assert(W % 4 == 0 && XV * 4 * kB2Threads >= W, "float4 slots cover the window");
     __shared__ __attribute__((aligned(16))) float xs[kXBuf][W];
     // Wide band2: + a scratch slot per lane (dummy lanes write there).  The other
@@ -298,9 +306,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     };
     // dma3: the loader wave's LDS-DMA of window q into buffer buf, W / 256 pieces of 1 KiB
     // (one wave-instruction each); only windows of the tile are issued.
+    auto wid_ld = [&]() { return (int)__builtin_amdgcn_readfirstlane(tid >> 6) - kLdWave; };
+    constexpr int kPieces = W / 256;
+    constexpr int kPpl = (kPieces + kNLd - 1) / kNLd;   // pieces per loader wave
     auto dma_win = [&](int32_t c, int32_t buf) {   // c: the window's first column
+        const int ld = kNLd > 1 ? wid_ld() : 0;
 #pragma unroll
-        for (int m = 0; m < W / 256; ++m) {
+        for (int k = 0; k < kPpl; ++k) {
+            const int m = ld + k * kNLd;
+            if (kPieces % kNLd != 0 && m >= kPieces) break;   // wave-uniform
             const uint32_t voff = 4u * (uint32_t)(c + m * 256 + lane * 4);
             const uint32_t lds = __builtin_amdgcn_readfirstlane(xs_lds + 4u * (uint32_t)(buf * W + m * 256));
             uint32_t keep;
@@ -325,13 +339,22 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     };
     // Entries of band q: band2 {word 2w, word 2w+1, value 2w, value 2w+1}, cband
     // {word 2w, word 2w+1} for this lane; past the tile: zeros = dummies.
-    using EV = typename std::conditional<CB, typename std::conditional<CPW == 3, u32x3, u32x2>::type, u32x4>::type;
+    using EV = typename std::conditional<
+        CB, typename std::conditional<CPW == 6, u32x8, typename std::conditional<CPW == 3, u32x3, u32x2>::type>::type,
+        u32x4>::type;
     auto load_e = [&](int32_t q) -> EV {
         const uint32_t off = (kApplyThreads < kB2Threads && tid >= kApplyThreads)
                                  ? 0xFFFFFFF0u
                                  : kBandBytes * (uint32_t)q + (kBandBytes / kApplyThreads) * (uint32_t)tid;
         if (ABL & 4) return EV{};
-        if constexpr (CB && CPW == 3)
+        if constexpr (CB && CPW == 6) {   // 24 bytes per lane: 16 + 8
+            const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, SM_ENT_AUX);
+            const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(e_src, off >= 0xFFFFFFF0u ? off : off + 16u, 0,
+                                                                 SM_ENT_AUX);
+            EV r;
+            r.s0 = a.x; r.s1 = a.y; r.s2 = a.z; r.s3 = a.w; r.s4 = b.x; r.s5 = b.y; r.s6 = 0u; r.s7 = 0u;
+            return r;
+        } else if constexpr (CB && CPW == 3)
             return __builtin_amdgcn_raw_buffer_load_b96(e_src, off, 0, SM_ENT_AUX);
         else if constexpr (CB)
             return __builtin_amdgcn_raw_buffer_load_b64(e_src, off, 0, SM_ENT_AUX);
@@ -461,7 +484,10 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     auto cb_finish = [&](CbState st) {
         float *xv = st.xv, *yv = st.yv, *tv = st.tv;
         // Materialise all reads before any write (one LDS wait per band).
-        if constexpr (CPW == 3)
+        if constexpr (CPW > 3) {
+#pragma unroll
+            for (int k = 0; k < CPW; ++k) asm volatile("" : "+v"(xv[k]), "+v"(yv[k]), "+v"(tv[k]));
+        } else if constexpr (CPW == 3)
             asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(xv[2]), "+v"(yv[0]), "+v"(yv[1]), "+v"(yv[2]),
                          "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]));
         else
@@ -511,9 +537,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     if constexpr (kLd) {
 #pragma unroll
         for (int v = 0; v < AE; ++v) E[v] = load_e(v);
-        if (wid == kLdWave) {   // windows 0 and 1; waited for (with everything) below
+        if (wid >= kLdWave) {   // windows 0 and 1 (dmaw: 0); waited for (with everything) below
             if (nb > 0) dma_win(clg[0], 0);
-            if (nb > 1) dma_win(clg[1], 1);
+            if (!kW && nb > 1) dma_win(clg[1], 1);
         }
     } else if constexpr (kDma) {
 #pragma unroll
@@ -587,7 +613,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             *reinterpret_cast<float4 *>(&yacc[4 * (tid + q * kB2Threads)]) = make_float4(-0.f, -0.f, -0.f, -0.f);
     }
     if constexpr (kLd) {
-        if (wid == kLdWave) {
+        if (wid >= kLdWave) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if constexpr (kXpf)
                 if (lane == 0) __hip_atomic_store(&s_xready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -611,7 +637,39 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t nbu = (ABL & 16) ? 0 : (nb + U - 1) / U * U;
     mark_phase(0);
     if constexpr (kProfLd) ph[0] = 0;   // the prologue is not a band phase
-    if constexpr (kLd) {
+    if constexpr (kW) {
+        if (wid >= kLdWave) {
+            // dmaw, band q: window q+1 into the buffer window q-1 left (every wave passed band
+            // q-1's barrier), wait until this wave's pieces of it have landed, meet the others
+            // at the barrier.  The windows' first columns come by scalar loads one band ahead.
+            int32_t c_next = nb > 1 ? clg[1] : 0;
+            __builtin_amdgcn_s_setprio(SM_LD_PRIO);
+            for (int32_t q = 0; q < nb; ++q) {
+                if (q + 1 < nb) {
+                    const int32_t c = c_next;
+                    const int32_t qn = __builtin_amdgcn_readfirstlane(q + 2);
+                    if (qn < nb) c_next = clg[qn];
+                    dma_win(c, (q + 1) & 1);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if constexpr (!(ABL & 512)) __syncthreads();
+            }
+        } else {
+            for (int32_t p = 0; p < nbu; p += U) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t q = p + u;
+                    if constexpr (ABL & 1) {
+                        asm volatile("" ::"v"(E[u % ER].s0), "v"(E[u % ER].s1));
+                    } else {
+                        apply_cb(xs[u % kXBuf], E[u % ER]);
+                    }
+                    E[u % ER] = load_e(q + AE);
+                    if (!(ABL & 512) && q < nb) __syncthreads();
+                }
+            }
+        }
+    } else if constexpr (kLd) {
         if (wid == kLdWave) {
             // Band q: DMA window q+2 into the buffer window q-1 left (every wave passed
             // band q-1's barrier), then wait until window q+1 has landed -- the 30 pieces
@@ -804,9 +862,10 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     const bool dma3 = xb.band_cols == kB2Dma3Cb.window;   // cband or band2 entries
     const bool dma3t = cb && xb.band_cols == kB2Dma3tCb.window;
     const bool dma3tall = cb && xb.band_cols == kB2Dma3TallCb.window;
-    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && !dma3tall && xb.band_cols != kB2Wide.window;
+    const bool dmaw = cb && xb.band_cols == kB2DmawCb.window;
+    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && !dma3tall && !dmaw && xb.band_cols != kB2Wide.window;
     const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? (cb ? kB2Dma3Cb : kB2Dma3B2) : dma3t ? kB2Dma3tCb
-                   : dma3tall ? kB2Dma3TallCb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+                   : dma3tall ? kB2Dma3TallCb : dmaw ? kB2DmawCb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -846,6 +905,15 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     if (dma3t) {
         if (abl != 0) return hipErrorInvalidValue;
         SM_B2(0, 2, true, 5);
+        return hipGetLastError();
+    }
+    if (dmaw && abl != 2048) {
+        switch (abl) {
+        case 0: SM_B2(0, 2, true, 8); break;
+        case 1: SM_B2(1, 2, true, 8); break;
+        case 8: SM_B2(8, 2, true, 8); break;
+        default: return hipErrorInvalidValue;
+        }
         return hipGetLastError();
     }
     if (dma3tall && abl != 2048) {
@@ -953,6 +1021,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             void *sym = nullptr;
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
             if (dma3) SM_B2(2048, 2, true, 4);
+            else if (dmaw) SM_B2(2048, 2, true, 8);
             else if (dma3tall) SM_B2(2048, 2, true, 6);
             else SM_B2(2048, 2, true, 0);
             (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
@@ -1008,6 +1077,8 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         SM_B2(0, 2, true, 5);
     } else if (dma3tall) {
         SM_B2(0, 2, true, 6);
+    } else if (dmaw) {
+        SM_B2(0, 2, true, 8);
     } else if (tall) {
         if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {

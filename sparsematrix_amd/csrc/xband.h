@@ -148,6 +148,13 @@ constexpr B2Geom kB2Dma3tCb{1 << 14, 7168, 13, 2, 13, 8, 30};
 // (waves 0-9 apply, 10-14 idle at the barriers), 12-bit columns and 11-bit row offsets (a chunk's
 // rows span < 2048).
 constexpr B2Geom kB2Dma3TallCb{1 << 15, 2560, 13, 2, 12, 1, 20};
+// dmaw (cband only; round 5): eight loader waves (8-15) stage 11520-column (45 KiB) windows by
+// LDS-DMA into TWO buffers, window q+1 issued at band q; waves 0-7 apply six chunks each of
+// 48-chunk bands, their entries four bands ahead.  One loader wave issues LDS-DMA at ~50 GB/s
+// per CU, two at ~95, four or more at ~113-117 (profiles/r05_xstream_flow.txt), and wider
+// windows cut the bands per tile from 36 to 23.  14-bit columns, 9-bit row offsets (a chunk's
+// rows span < 512).  LDS: 2 x 45 KiB + 64 KiB + 4 table copies = 158 KiB.
+constexpr B2Geom kB2DmawCb{1 << 14, 11520, 14, 6, 14, 4, 48};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)
@@ -165,8 +172,10 @@ struct Band2Host {
 // Returns false when the layout does not apply: unsorted columns or size limits
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
 // ids != nullptr builds the cband encoding: ids[e] = codebook id (< 255) of term e.
-// slab0_permille: slab 0's columns as a share of an even split (1000 = even slabs).
-constexpr int32_t kB2Slab0Permille = 930;
+// slab0_permille: slab 0's columns as a share of an even split (1000 = even slabs).  AUTO keeps
+// even slabs: narrower slab-0 tiles measured 900: 34.0-34.2, 930: 34.1, 960: 32.9-33.2,
+// 1000: 33.3-33.4 us on config 2 (profiles/r05_slab0_ab.txt).
+constexpr int32_t kB2Slab0Permille = 1000;
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
                  B2Geom geom = kB2Wide, int32_t slab0_permille = 1000);

@@ -189,7 +189,8 @@ static int check_random(int64_t n_rows, int64_t n_cols, int per_row, unsigned se
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2TallCb);
         bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Wide3Cb);
         // the AUTO geometry (dma3) with slab 0 narrower, as sm_create_* builds it
-        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Dma3Cb, kB2Slab0Permille);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2Dma3Cb, 930);
+        bad += check_layout_cb(rp, col, val, n_rows, n_cols, slabs, kB2DmawCb);   // six chunks per wave
     }
     return bad;
 }

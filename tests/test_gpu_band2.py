@@ -47,8 +47,8 @@ def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
 def _skip_geometry(kind, tall):
     if (tall == 6 and kind == "band2") or (tall == 4 and kind == "cband"):
         pytest.skip("the same geometry as tall = 0")
-    if tall == 7 and kind == "band2":
-        pytest.skip("dma3 tall is a codebook-word geometry")
+    if tall in (7, 8) and kind == "band2":
+        pytest.skip("dma3 tall and dmaw are codebook-word geometries")
 
 
 def _check(M, info, rp, ci, va, x, y0, alpha, beta, algo="xband"):
@@ -72,7 +72,7 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
 def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
     """tall: 0 the default (cband: dma3), 1 tall, 4 dma3 (band2's 8-byte entries in it), 6 wide,
     7 dma3 tall (codebook words only)."""
@@ -135,7 +135,7 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
 def test_band2_special_values_and_signed_zeros(sm, kind, tall):
     _skip_geometry(kind, tall)
     n_rows, n_cols = 30000, 50000
@@ -164,7 +164,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
 def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
@@ -186,6 +186,25 @@ def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
         assert np.array_equal(bits(to_host(y)), first)
     want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
     assert np.array_equal(first, bits(want))
+
+
+@pytest.mark.parametrize("kind", list(KINDS))
+@pytest.mark.parametrize("permille", [900, 960])
+def test_band2_narrow_slab0_vs_oracle(sm, kind, permille):
+    """sm_build_opts.band_slab0_permille: slab 0 narrower than the even share, the other
+    slabs split the rest; bit-identical to the slab-order restatement on the reported
+    boundaries (sm_info.xband_slab0_cols / xband_slab_cols)."""
+    n_rows, n_cols = 200003, 300001
+    rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=41)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout=kind, band_slab0_permille=permille))
+    info = M.info()
+    assert info["has_xband"] == KINDS[kind] and info["xband_slabs"] > 1, info
+    assert info["xband_slab0_cols"] < info["xband_slab_cols"], info
+    assert info["xband_slab0_cols"] + (info["xband_slabs"] - 1) * info["xband_slab_cols"] >= n_cols, info
+    rng = np.random.default_rng(42)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
+    _check(M, info, rp, ci, va, x, y0, 1.3, 0.7)
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
@@ -298,13 +317,15 @@ def test_cband_dma3_special_values_and_repeats(sm):
         assert np.array_equal(bits(to_host(y)), bits(want))
 
 
-def test_cband_dma3_config2_vs_slab_oracle(sm):
-    """Config 2 in the dma3 geometry: bit-identical to the 4-slab restatement."""
+@pytest.mark.parametrize("tall", [4, 8])
+def test_cband_dma3_config2_vs_slab_oracle(sm, tall):
+    """Config 2 in the dma3 geometry (tall 4) and in dmaw (tall 8: eight loader waves, two
+    45 KiB windows, 48-chunk bands): bit-identical to the 4-slab restatement."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
-    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=4))
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=tall))
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_block_rows"] == 16384, info
     g = torch.Generator(device="cuda").manual_seed(9)
@@ -319,14 +340,14 @@ def test_cband_dma3_config2_vs_slab_oracle(sm):
 
 def test_band2_config2_equals_blocked(sm):
     """BASELINE config 2 (2^20 x 2^20, 16 terms/row): cband, band2 and the blocked kind
-    built on the same 4 even slabs of 262144 columns (band_slab0_permille = 1000; AUTO makes
-    slab 0 narrower) sum each in the reference's order, so their results are bit-identical."""
+    built on the same 4 even slabs of 262144 columns sum each in the reference's order, so
+    their results are bit-identical."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     n = 1 << 20
     rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
-    Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(band_slab0_permille=1000))
-    Mb2 = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="band2", band_slab0_permille=1000))
+    Mcb = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    Mb2 = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="band2"))
     Mbl = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="blocked"))
     ic, i2, ib = Mcb.info(), Mb2.info(), Mbl.info()
     assert ic["has_xband"] == 5 and i2["has_xband"] == 4 and ib["has_xband"] == 2
@@ -413,8 +434,7 @@ def test_config2_auto_full_size_vs_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n)
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_slabs"] == 4, info
-    # slab 0 narrower (kB2Slab0Permille), the other three share the rest
-    assert info["xband_slab0_cols"] == 243968 and info["xband_slab_cols"] == 268288, info
+    assert info["xband_slab0_cols"] == info["xband_slab_cols"] == 262144, info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
