@@ -340,9 +340,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // us for the wide geometry with codebook words, 37.9-38.0 vs 38.6-38.7 with 8-byte
     // entries); band_tall = 6 keeps the wide one.
     if (geo_opt == 0) geo_opt = 4;   // dma3 for codebook words and 8-byte entries alike
-    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7 || geo_opt == 8) && kind == kXbCband);
+    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7 || geo_opt == 8 || geo_opt == 9) && kind == kXbCband);
     const B2Geom geom = half2 ? kB2Half2Cb
-                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb : geo_opt == 8 ? kB2DmawCb
+                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb : geo_opt == 8 ? kB2DmawCb : geo_opt == 9 ? kB2Dmaw4Cb
                                 : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
                       : !tall ? kB2Wide
                       : kind == kXbCband ? kB2TallCb : kB2TallB2;
@@ -361,9 +361,9 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     const bool wide3 = false;
 #endif
     B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
-    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7 || geo_opt == 8) {   // half2 / dma3* / dmaw: codebook words
+    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7 || geo_opt == 8 || geo_opt == 9) {   // half2 / dma3* / dmaw: codebook words
         if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : geo_opt == 5 ? kB2Dma3tCb
-                    : geo_opt == 8 ? kB2DmawCb : kB2Dma3TallCb;
+                    : geo_opt == 8 ? kB2DmawCb : geo_opt == 9 ? kB2Dmaw4Cb : kB2Dma3TallCb;
         else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
         else return SM_OK;                    // a codebook-only geometry was asked for
     }
@@ -417,6 +417,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
     d.slab0_cols = bh.slab0_cols;
+    d.chunks_per_wave = g.cpw;
     d.n_chunks = bh.n_bands * g.chunks();
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;

@@ -134,14 +134,15 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     static_assert(GEO < 2 || GEO == 4 || CB, "wide3, half2, dma3t and dma3 tall are cband geometries");
     constexpr B2Geom G = TALL ? (CB ? kB2TallCb : kB2TallB2) : GEO == 2 ? kB2Wide3Cb
                        : GEO == 3 ? kB2Half2Cb : GEO == 4 ? (CB ? kB2Dma3Cb : kB2Dma3B2)
-                       : GEO == 5 ? kB2Dma3tCb : GEO == 6 ? kB2Dma3TallCb : GEO == 8 ? kB2DmawCb : kB2Wide;
-    static_assert(GEO != 8 || CB, "dmaw is a codebook geometry");
+                       : GEO == 5 ? kB2Dma3tCb : GEO == 6 ? kB2Dma3TallCb : GEO == 8 ? kB2DmawCb
+                       : GEO == 9 ? kB2Dmaw4Cb : kB2Wide;
+    static_assert(GEO < 8 || CB, "dmaw is a codebook geometry");
     // dma3: wave kLdWave stages the x windows (LDS-DMA, three buffers, two bands ahead) and
     // the other waves apply -- no x ever passes through an applying wave's registers, and
     // the loader's wait for its DMA is the only vmcnt wait on x (its queue holds nothing else).
-    constexpr bool kLd = GEO == 4 || GEO == 5 || GEO == 6 || GEO == 8;
-    constexpr bool kW = GEO == 8;                         // dmaw: 8 loader waves, two x buffers
-    constexpr int kNLd = kW ? 8 : 1;                      // loader waves (the last ones)
+    constexpr bool kLd = GEO == 4 || GEO == 5 || GEO == 6 || GEO == 8 || GEO == 9;
+    constexpr bool kW = GEO == 8 || GEO == 9;             // dmaw: several loader waves, two x buffers
+    constexpr int kNLd = kW ? 16 - G.chunks() / G.cpw : 1;   // loader waves (the last ones)
     constexpr int kLdWave = kB2Threads / 64 - kNLd;       // the first loader wave
     constexpr int CPW = CB ? G.cpw : 2;   // chunks per wave per band
     constexpr int BROWS = G.block_rows;
@@ -340,7 +341,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // Entries of band q: band2 {word 2w, word 2w+1, value 2w, value 2w+1}, cband
     // {word 2w, word 2w+1} for this lane; past the tile: zeros = dummies.
     using EV = typename std::conditional<
-        CB, typename std::conditional<CPW == 6, u32x8, typename std::conditional<CPW == 3, u32x3, u32x2>::type>::type,
+        CB, typename std::conditional<CPW == 6, u32x8,
+                typename std::conditional<CPW == 4, u32x4,
+                        typename std::conditional<CPW == 3, u32x3, u32x2>::type>::type>::type,
         u32x4>::type;
     auto load_e = [&](int32_t q) -> EV {
         const uint32_t off = (kApplyThreads < kB2Threads && tid >= kApplyThreads)
@@ -354,6 +357,8 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             EV r;
             r.s0 = a.x; r.s1 = a.y; r.s2 = a.z; r.s3 = a.w; r.s4 = b.x; r.s5 = b.y; r.s6 = 0u; r.s7 = 0u;
             return r;
+        } else if constexpr (CB && CPW == 4) {
+            return __builtin_amdgcn_raw_buffer_load_b128(e_src, off, 0, SM_ENT_AUX);
         } else if constexpr (CB && CPW == 3)
             return __builtin_amdgcn_raw_buffer_load_b96(e_src, off, 0, SM_ENT_AUX);
         else if constexpr (CB)
@@ -649,23 +654,36 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                     const int32_t c = c_next;
                     const int32_t qn = __builtin_amdgcn_readfirstlane(q + 2);
                     if (qn < nb) c_next = clg[qn];
+                    if constexpr (kProfLd) mark_phase(5);
                     dma_win(c, (q + 1) & 1);
+                    if constexpr (kProfLd) mark_phase(3);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
+                if constexpr (kProfLd) mark_phase(4);
                 if constexpr (!(ABL & 512)) __syncthreads();
+                if constexpr (kProfLd) mark_phase(5);
             }
         } else {
             for (int32_t p = 0; p < nbu; p += U) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int32_t q = p + u;
+                    if constexpr (kProfLd) {
+                        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((CPW == 6 ? 2 : 1) * (AE - 1)) : "memory");
+                        mark_phase(0);
+                    }
                     if constexpr (ABL & 1) {
                         asm volatile("" ::"v"(E[u % ER].s0), "v"(E[u % ER].s1));
                     } else {
                         apply_cb(xs[u % kXBuf], E[u % ER]);
                     }
+                    if constexpr (kProfLd) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        mark_phase(1);
+                    }
                     E[u % ER] = load_e(q + AE);
                     if (!(ABL & 512) && q < nb) __syncthreads();
+                    if constexpr (kProfLd) mark_phase(2);
                 }
             }
         }
@@ -822,7 +840,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         }
         if constexpr (kProfLd) {   // [6] bands, [7] applying waves (the loader adds 1 << 32)
             ph[6] = (unsigned long long)nb;
-            ph[7] = wid == kLdWave ? (1ull << 32) : 1ull;
+            ph[7] = wid >= kLdWave ? (1ull << 32) : 1ull;
             if (lane == 0)
                 for (int k = 0; k < 8; ++k) atomicAdd(&g_b2_prof[k], ph[k]);
         }
@@ -862,10 +880,12 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
     const bool dma3 = xb.band_cols == kB2Dma3Cb.window;   // cband or band2 entries
     const bool dma3t = cb && xb.band_cols == kB2Dma3tCb.window;
     const bool dma3tall = cb && xb.band_cols == kB2Dma3TallCb.window;
-    const bool dmaw = cb && xb.band_cols == kB2DmawCb.window;
-    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && !dma3tall && !dmaw && xb.band_cols != kB2Wide.window;
+    const bool dmaw_any = cb && xb.band_cols == kB2DmawCb.window;
+    const bool dmaw4 = dmaw_any && xb.kind == kXbCband && xb.chunks_per_wave == 4;
+    const bool dmaw = dmaw_any && !dmaw4;
+    const bool tall = !wide3 && !half2 && !dma3 && !dma3t && !dma3tall && !dmaw_any && xb.band_cols != kB2Wide.window;
     const B2Geom g = wide3 ? kB2Wide3Cb : half2 ? kB2Half2Cb : dma3 ? (cb ? kB2Dma3Cb : kB2Dma3B2) : dma3t ? kB2Dma3tCb
-                   : dma3tall ? kB2Dma3TallCb : dmaw ? kB2DmawCb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
+                   : dma3tall ? kB2Dma3TallCb : dmaw ? kB2DmawCb : dmaw4 ? kB2Dmaw4Cb : tall ? (cb ? kB2TallCb : kB2TallB2) : kB2Wide;
     if ((xb.kind != kXbBand2 && !cb) || xb.n_slabs < 1 || xb.block_rows > g.block_rows ||
         xb.band_cols != g.window || !xb.d_chunk_start || !xb.d_band_clo ||
         (xb.n_bands > 0 && !xb.d_word) ||
@@ -907,8 +927,43 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         SM_B2(0, 2, true, 5);
         return hipGetLastError();
     }
+    if (dmaw4 && abl != 2048) {
+        if (abl == 0) SM_B2(0, 2, true, 9);
+        else if (abl == 4096) {
+            unsigned long long h[8] = {};
+            void *sym = nullptr;
+            if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_prof)) != hipSuccess) return hipErrorInvalidValue;
+            (void)hipMemsetAsync(sym, 0, sizeof(h), s);
+            SM_B2(4096, 2, true, 9);
+            (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double wa = (double)(h[7] & 0xFFFFFFFFull), wl = (double)(h[7] >> 32);
+            const double bands = (double)h[6] / (wa + wl);
+            fprintf(stderr, "dmaw4 prof (cycles per band per wave; %.0f applying + %.0f loader waves, %.1f bands): "
+                    "apply waves: entry wait %.0f apply %.0f barrier %.0f | loaders: issue %.0f dma wait %.0f "
+                    "barrier %.0f\n", wa, wl, bands, h[0] / wa / bands, h[1] / wa / bands, h[2] / wa / bands,
+                    h[3] / wl / bands, h[4] / wl / bands, h[5] / wl / bands);
+        } else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (dmaw && abl != 2048) {
         switch (abl) {
+        case 4096: {
+            unsigned long long h[8] = {};
+            void *sym = nullptr;
+            if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_prof)) != hipSuccess) return hipErrorInvalidValue;
+            (void)hipMemsetAsync(sym, 0, sizeof(h), s);
+            SM_B2(4096, 2, true, 8);
+            (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
+            (void)hipStreamSynchronize(s);
+            const double wa = (double)(h[7] & 0xFFFFFFFFull), wl = (double)(h[7] >> 32);
+            const double bands = (double)h[6] / (wa + wl);
+            fprintf(stderr, "dmaw prof (cycles per band per wave; %.0f applying + %.0f loader waves, %.1f bands): "
+                    "apply waves: entry wait %.0f apply %.0f barrier %.0f | loaders: issue %.0f dma wait %.0f "
+                    "barrier %.0f\n", wa, wl, bands, h[0] / wa / bands, h[1] / wa / bands, h[2] / wa / bands,
+                    h[3] / wl / bands, h[4] / wl / bands, h[5] / wl / bands);
+            break;
+        }
         case 0: SM_B2(0, 2, true, 8); break;
         case 1: SM_B2(1, 2, true, 8); break;
         case 8: SM_B2(8, 2, true, 8); break;
@@ -1022,6 +1077,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
             if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
             if (dma3) SM_B2(2048, 2, true, 4);
             else if (dmaw) SM_B2(2048, 2, true, 8);
+            else if (dmaw4) SM_B2(2048, 2, true, 9);
             else if (dma3tall) SM_B2(2048, 2, true, 6);
             else SM_B2(2048, 2, true, 0);
             (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
@@ -1079,6 +1135,8 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
         SM_B2(0, 2, true, 6);
     } else if (dmaw) {
         SM_B2(0, 2, true, 8);
+    } else if (dmaw4) {
+        SM_B2(0, 2, true, 9);
     } else if (tall) {
         if (cb) SM_B2(0, 2, true, 1); else SM_B2(0, 2, false, 1);
     } else {

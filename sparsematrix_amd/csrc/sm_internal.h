@@ -75,6 +75,7 @@ struct XbandDev {
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int32_t n_slabs = 1, slab_bands = 0;   // tiles = n_blocks * n_slabs
     int32_t slab0_cols = 0;           // band2 / cband: columns of slab 0 (others: slab_bands)
+    int32_t chunks_per_wave = 2;      // band2 / cband: the geometry's chunks per applying wave
     int64_t n_chunks = 0;
     int64_t max_chunks_per_band = 0;
     int32_t *d_chunk_start = nullptr;

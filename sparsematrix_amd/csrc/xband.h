@@ -155,6 +155,8 @@ constexpr B2Geom kB2Dma3TallCb{1 << 15, 2560, 13, 2, 12, 1, 20};
 // windows cut the bands per tile from 36 to 23.  14-bit columns, 9-bit row offsets (a chunk's
 // rows span < 512).  LDS: 2 x 45 KiB + 64 KiB + 4 table copies = 158 KiB.
 constexpr B2Geom kB2DmawCb{1 << 14, 11520, 14, 6, 14, 4, 48};
+// dmaw4: the same windows, four loader waves (12-15) and twelve applying waves of four chunks.
+constexpr B2Geom kB2Dmaw4Cb{1 << 14, 11520, 14, 4, 14, 4, 48};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

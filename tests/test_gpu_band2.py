@@ -47,7 +47,7 @@ def _band2(sm, rp, ci, va, n_cols, slabs=None, kind="band2", tall=0):
 def _skip_geometry(kind, tall):
     if (tall == 6 and kind == "band2") or (tall == 4 and kind == "cband"):
         pytest.skip("the same geometry as tall = 0")
-    if tall in (7, 8) and kind == "band2":
+    if tall in (7, 8, 9) and kind == "band2":
         pytest.skip("dma3 tall and dmaw are codebook-word geometries")
 
 
@@ -72,7 +72,7 @@ SHAPES = [(200003, 300001, 16), (9000, 70001, 40), (5000, 1000, 5), (40000, 2000
 @pytest.mark.parametrize("n_rows,n_cols,per_row", SHAPES)
 @pytest.mark.parametrize("slabs", [1, None])
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8, 9])
 def test_band2_vs_oracle(sm, n_rows, n_cols, per_row, slabs, kind, tall):
     """tall: 0 the default (cband: dma3), 1 tall, 4 dma3 (band2's 8-byte entries in it), 6 wide,
     7 dma3 tall (codebook words only)."""
@@ -135,7 +135,7 @@ def test_band2_ragged_rows_and_empty_regions(sm, kind):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8, 9])
 def test_band2_special_values_and_signed_zeros(sm, kind, tall):
     _skip_geometry(kind, tall)
     n_rows, n_cols = 30000, 50000
@@ -164,7 +164,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
 
 
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8])
+@pytest.mark.parametrize("tall", [0, 1, 4, 6, 7, 8, 9])
 def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     """Back-to-back SpMVs on one stream: the slab hand-off's control words return to
     zero after every launch, so repeated products are bit-identical."""
@@ -317,7 +317,7 @@ def test_cband_dma3_special_values_and_repeats(sm):
         assert np.array_equal(bits(to_host(y)), bits(want))
 
 
-@pytest.mark.parametrize("tall", [4, 8])
+@pytest.mark.parametrize("tall", [4, 8, 9])
 def test_cband_dma3_config2_vs_slab_oracle(sm, tall):
     """Config 2 in the dma3 geometry (tall 4) and in dmaw (tall 8: eight loader waves, two
     45 KiB windows, 48-chunk bands): bit-identical to the 4-slab restatement."""
@@ -385,7 +385,7 @@ def test_band2_tall_config2_vs_slab_oracle(sm, kind):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout=kind, band_tall=1))
     info = M.info()
     assert info["has_xband"] == KINDS[kind] and info["xband_block_rows"] == 32768, info
-    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] < info["xband_slab_cols"], info
+    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] == info["xband_slab_cols"] == 131072, info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
@@ -407,7 +407,7 @@ def test_cband_dma3_tall_config2_vs_slab_oracle(sm):
     M = sm.SparseMatrix.from_csr(rp, ci, va, n, opts=dict(layout="cband", band_tall=7))
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_block_rows"] == 32768, info
-    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] < info["xband_slab_cols"], info
+    assert info["xband_slabs"] == 8 and info["xband_slab0_cols"] == info["xband_slab_cols"] == 131072, info
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
