@@ -120,7 +120,8 @@ typedef struct sm_info {
     int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
                                    2 blocked, 3 gather, 4 band2 (balanced bands),
                                    5 cband (balanced bands, codebook words),
-                                   6 gcb (gathered chunk bands);
+                                   6 gcb (gathered chunk bands), 7 ro (row-owner
+                                   codebook bands, band_tall = 10);
                                    2-6 sum each column slab in the reference's
                                    order and add the slab sums in slab order     */
     int32_t xband_blocks, xband_bands;

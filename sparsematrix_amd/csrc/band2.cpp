@@ -31,9 +31,7 @@ struct TileOut {
     bool ok = true;
 };
 
-struct Seg {
-    int32_t rl, s, n;   // row in block, first term, count
-};
+using Seg = B2Seg;
 
 // Lanes inside a chunk: segments of 2+ terms take consecutive lanes first (the
 // kernel passes a running sum up the lanes), then the single terms go to the two
@@ -368,6 +366,16 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
 }
 
 }  // namespace
+
+void b2_emit_chunk(uint32_t *band_ent, int c, const std::vector<B2Seg> &segs, const int32_t *col,
+                   const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom) {
+    emit_chunk(band_ent, c, segs, col, val, ids, clo_al, geom);
+}
+
+void b2_balance_chunks(std::vector<std::vector<B2Seg>> &cs, int nc, const int32_t *col, int32_t clo_al,
+                       int32_t span) {
+    balance_chunks(cs, nc, col, clo_al, span);
+}
 
 bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids, B2Geom geom,

@@ -21,6 +21,7 @@
 #include "sm_internal.h"
 #include "sell.h"
 #include "xband.h"
+#include "ro.h"
 
 using namespace smamd;
 
@@ -424,8 +425,56 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     return SM_OK;
 }
 
+// Row-owner codebook bands (ro.h, kernels_ro.hip; band_tall = 10): applying waves own rows,
+// no barrier between windows.
+static sm_status upload_ro(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    std::vector<float> table;
+    std::vector<uint8_t> ids;
+    if (!codebook_ids(val, m->nnz, table, ids)) return SM_OK;
+    const int64_t nblk = (m->n_rows + kRoBlockRows - 1) / kRoBlockRows;
+    int32_t slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
+    if (m->opts.band_slabs > 0) slabs = m->opts.band_slabs;
+    RoHost h;
+    if (!ro_build(rp, col, ids.data(), m->n_rows, m->n_cols, slabs, h)) return SM_OK;
+    std::vector<uint8_t>().swap(ids);
+    XbandDev &d = m->plan.xb;
+    const int64_t ntile = (int64_t)h.n_blocks * h.n_slabs;
+    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile * kRoApplyWaves + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, h.n_chunks * 64), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
+    SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
+    if (!table.empty())
+        SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
+    d.table_size = (int32_t)table.size();
+    if (h.n_slabs > 1) {
+        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;
+        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(h.n_slabs - 1) * ps, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)h.n_blocks, m->device_bytes));
+        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)h.n_blocks * 4 * sizeof(int32_t)));
+    }
+    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, h.wave_start.data(), h.wave_start.size() * 4, hipMemcpyHostToDevice));
+    if (h.n_chunks > 0)
+        SM_TRY_HIP(hipMemcpy(d.d_word, h.ent.data(), (size_t)h.n_chunks * 256, hipMemcpyHostToDevice));
+    d.kind = kXbRo;
+    d.threads = 1024;
+    d.block_rows = h.block_rows;
+    d.band_cols = kRoWindow;
+    d.n_bands = (int32_t)std::min<int64_t>(h.n_chunks, INT32_MAX);   // chunks
+    d.n_slabs = h.n_slabs;
+    d.slab_bands = h.slab_cols;
+    d.slab0_cols = h.slab_cols;
+    d.n_chunks = h.n_chunks;
+    d.max_chunks_per_band = h.max_chunks_per_wave;
+    d.n_blocks = h.n_blocks;
+    return SM_OK;
+}
+
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
+    if (kind == kXbCband && m->opts.band_tall == 10) {
+        const sm_status st = upload_ro(m, rp, col, val);
+        if (st != SM_OK || m->plan.xb.n_blocks > 0) return st;
+    }
     // Geometry: band_tall (xband.h B2Geom, build_band2).
     // Slab 0's tile loads and scales y (64 KiB per 16K-row block from HBM) before its first
     // band: on config 2 its band loop ended 1.5-2.3 us after the other slabs' (per-tile
@@ -1468,7 +1517,7 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
 sm_status sm_debug_seed_handoff(sm_matrix *m, uint64_t started) {
     if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
     const XbandDev &xb = m->plan.xb;
-    if (xb.n_blocks <= 0 || (xb.kind != kXbBand2 && xb.kind != kXbCband) || xb.n_slabs < 2 || !xb.d_tickets)
+    if (xb.n_blocks <= 0 || (xb.kind != kXbBand2 && xb.kind != kXbCband && xb.kind != kXbRo) || xb.n_slabs < 2 || !xb.d_tickets)
         return fail(SM_ERR_NOT_SUPPORTED, "no multi-slab band2/cband layout");
     if (started % (uint64_t)xb.n_slabs != 0)
         return fail(SM_ERR_NOT_SUPPORTED, "started must be a multiple of the slab count");
@@ -1506,7 +1555,8 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->xband_block_rows = m->plan.xb.block_rows;
     info->xband_slab_cols =
         m->plan.xb.n_blocks == 0 ? 0
-        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb
+        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb ||
+                  m->plan.xb.kind == kXbRo
             ? m->plan.xb.slab_bands   // band2 / cband / gcb keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->xband_slab0_cols = m->plan.xb.slab0_cols > 0 ? m->plan.xb.slab0_cols : info->xband_slab_cols;
@@ -1708,6 +1758,8 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
             e = m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
                     ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
+                : m->plan.xb.kind == kXbRo
+                    ? launch_spmv_ro(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                 : m->plan.xb.kind == kXbGcb
                     ? launch_spmv_gcb(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                     : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);

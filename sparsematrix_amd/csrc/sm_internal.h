@@ -231,6 +231,9 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
                            float alpha, float beta, hipStream_t s);
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
+// Row-owner codebook bands (ro.h, kernels_ro.hip): xb.kind == kXbRo.
+hipError_t launch_spmv_ro(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x, float *y,
+                          float alpha, float beta, hipStream_t s);
 // xp[rank[c]] = x[c], c < n (rank: original column -> new column).
 hipError_t launch_x_relabel(int64_t n, const int32_t *rank, const float *x, float *xp,
                             hipStream_t s);

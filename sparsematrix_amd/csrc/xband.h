@@ -28,7 +28,8 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
 //             column order so the x gathers of one wave-instruction hit a few cache
 //             lines; LDS holds only the accumulators (measured slower, kept for A/B).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5, kXbGcb = 6 };
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5, kXbGcb = 6,
+                        kXbRo = 7 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
@@ -181,6 +182,17 @@ constexpr int32_t kB2Slab0Permille = 1000;
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
                  B2Geom geom = kB2Wide, int32_t slab0_permille = 1000);
+
+// A row's run of terms inside one chunk: row in block, first term index, count.
+struct B2Seg {
+    int32_t rl, s, n;
+};
+// The band builder's chunk emitter (bank-aware lane placement, band2.cpp) and its cross-chunk
+// bank balance, for other builders of codebook chunks (ro.cpp): chunk c of a band slot.
+void b2_emit_chunk(uint32_t *band_ent, int c, const std::vector<B2Seg> &segs, const int32_t *col,
+                   const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom);
+void b2_balance_chunks(std::vector<std::vector<B2Seg>> &cs, int nc, const int32_t *col, int32_t clo_al,
+                       int32_t span);
 
 // Codebook of a value array: table[ids[e]] has the bits of val[e] for every e; false
 // when there are more than 255 distinct bit patterns (table then undefined).
