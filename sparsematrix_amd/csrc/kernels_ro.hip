@@ -5,7 +5,8 @@
 // through three 30 KiB LDS windows by LDS-DMA, the <= 255-entry table scaled by alpha in
 // LDS (4 copies), the slab hand-off of xband_dev.h.  Roles:
 //   waves 0..13 apply: wave w owns the block's rows [w * 1171, (w + 1) * 1171) and walks its
-//     own chunk stream (ro.cpp) two chunks at a time, in window order;
+//     own chunk stream (ro.cpp) two chunks at a time, in window order -- together when their
+//     rows are disjoint, else (kRoDepBit on the second) the first and then the second;
 //   waves 14..15 load: each issues half of every window's 30 1 KiB pieces.
 // No barrier between windows: a wave applies window q's chunks once both loaders have
 // published window q in LDS (ldp[] >= q + 1), and publishes prog[w] = q when it moves on to
@@ -32,6 +33,7 @@ constexpr int kRoPpl = (kRoPieces + kRoLoadWaves - 1) / kRoLoadWaves;   // 15
 constexpr int kRoAE = 3;                                          // entry pairs in flight
 constexpr int kRoTab = 4;                                         // table copies
 constexpr uint32_t kRoColMask = (1u << 13) - 1u;
+constexpr uint32_t kRoWinMask = (uint32_t)kRoMaxWindows - 1u;
 constexpr int kRoOffShift = 13 + kCbIdBits;                       // 21
 static_assert(kRoApplyWaves + kRoLoadWaves == kRoThreads / 64, "roles fill the workgroup");
 static_assert(kRoPieces % kRoLoadWaves == 0, "whole pieces per loader");
@@ -181,15 +183,16 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
             for (int u = 0; u < kRoAE; ++u) {
                 const int32_t pi = p0 + u;
                 if (pi < npair) {   // wave-uniform
-                    uint32_t wd[2], qk[2], base[2];
+                    uint32_t wd[2], qk[2], base[2], dep1 = 0;
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
                         wd[k] = E[u][k] ^ dmy;
                         const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
-                        qk[k] = h & kRoColMask;
+                        qk[k] = h & kRoWinMask;
                         base[k] = (uint32_t)wrow + (((h >> kRoOffShift) & kCbOffMask) | ((h >> kCbContBit) << 10));
+                        if (k == 1) dep1 = h & kRoDepBit;
                     }
-                    if (2 * pi + 1 >= nch) qk[1] = qk[0];   // past the stream: a dummy chunk
+                    if (2 * pi + 1 >= nch) { qk[1] = qk[0]; dep1 = 0; }   // past the stream: a dummy chunk
                     if ((int32_t)qk[0] > done_q) {   // moving on: windows < qk[0] are read in full
                         done_q = (int32_t)qk[0];
                         if (lane == 0) lds_st(&prog[wid], done_q);
@@ -200,14 +203,19 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                         if (ready <= (int32_t)qk[1]) __builtin_amdgcn_s_sleep(1);
                     }
                     __builtin_amdgcn_s_setprio(2);
+                    // together (one pass) unless the second chunk reads a row the first writes:
+                    // then pass 0 applies the first alone and pass 1 the second
+                    const int npass = dep1 ? 2 : 1;
+                    for (int ps = 0; ps < npass; ++ps) {
+                    const uint64_t on[2] = {(!dep1 || ps == 0) ? ~1ull : 0ull, (!dep1 || ps == 1) ? ~1ull : 0ull};
                     float xv[2], tv[2], yv[2];
                     uint32_t rl[2];
                     uint64_t live[2], cont[2];
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
                         const uint32_t id = (wd[k] >> 13) & kCbDummyId;
-                        live[k] = __ballot(id != kCbDummyId) & ~1ull;
-                        cont[k] = __ballot((int32_t)wd[k] < 0) & ~1ull;
+                        live[k] = __ballot(id != kCbDummyId) & on[k];
+                        cont[k] = __ballot((int32_t)wd[k] < 0) & on[k];
                         rl[k] = base[k] + ((wd[k] >> kRoOffShift) & kCbOffMask);
                         xv[k] = xs[qk[k] % kRoBufs][wd[k] & kRoColMask];
                         tv[k] = tab[id * kRoTab + (lane & (kRoTab - 1))];
@@ -233,6 +241,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                     for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
                         const uint64_t last = live[k] & ~(cont[k] >> 1);
                         if ((last >> lane) & 1) yacc[rl[k]] = acc[k];
+                    }
                     }
                     __builtin_amdgcn_s_setprio(0);
                 }

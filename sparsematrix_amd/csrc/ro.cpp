@@ -42,9 +42,11 @@ void build_tile(const int32_t *rp, const int32_t *col, const uint8_t *ids, int64
     std::vector<int32_t> cur, end;
     std::vector<B2Seg> segs;
     std::vector<std::vector<B2Seg>> cs;
+    std::vector<int32_t> prev_rows, rows;   // rows of the wave's previous chunk / this one (sorted)
     for (int w = 0; w < kRoApplyWaves; w++) {
         const int64_t wr0 = r0 + (int64_t)w * kRoWaveRows, wr1 = std::min<int64_t>(r1, wr0 + kRoWaveRows);
         if (wr0 >= wr1) continue;
+        prev_rows.clear();
         const int64_t nr = wr1 - wr0;
         cur.assign((size_t)nr, 0);
         end.assign((size_t)nr, 0);
@@ -92,9 +94,16 @@ void build_tile(const int32_t *rp, const int32_t *col, const uint8_t *ids, int64
                 const size_t at = out.ent.size();
                 out.ent.resize(at + 64, 0u);
                 b2_emit_chunk(out.ent.data() + at, 0, cs[(size_t)c], col, nullptr, ids, (int32_t)clo, kRoGeom);
-                // header: window index | base row relative to the wave's first row (11 bits)
+                // header: window index | dep | base row relative to the wave's first row (11 bits)
                 const uint32_t brel = (uint32_t)(cs[(size_t)c].front().rl - (int32_t)(wr0 - r0));
-                const uint32_t h = ((uint32_t)q & cmask) | dmy | ((brel & 1023u) << osh) | ((brel >> 10) << kCbContBit);
+                rows.clear();
+                for (const B2Seg &g : cs[(size_t)c]) rows.push_back(g.rl);
+                std::sort(rows.begin(), rows.end());
+                bool dep = false;
+                for (int32_t r : rows) dep = dep || std::binary_search(prev_rows.begin(), prev_rows.end(), r);
+                prev_rows.swap(rows);
+                const uint32_t h = ((uint32_t)q & (cmask >> 1)) | (dep ? kRoDepBit : 0u) | dmy | ((brel & 1023u) << osh) |
+                                   ((brel >> 10) << kCbContBit);
                 out.ent[at] = h ^ dmy;
             }
             out.wave_chunks[(size_t)w] += nc;

@@ -13,8 +13,11 @@
 //
 // Entry word (stored XOR kCbDummyWord, zero = dummy): column - window start (13 bits) |
 // codebook id (8) | row - chunk base (10) | continuation (1), as cband.  Header (lane 0):
-// id 255, column field = the window index, row field + continuation bit = the chunk's base
-// row relative to the wave's first row (11 bits).
+// id 255; column field = the window index (bits 0-11) | kRoDepBit (the chunk shares a row
+// with the previous chunk of the wave's stream: a row cut in 63-term pieces, or a row with
+// terms in both windows); row field + continuation bit = the chunk's base row relative to
+// the wave's first row (11 bits).  The kernel applies two consecutive chunks together unless
+// the second carries kRoDepBit; then in turn (the second reads the first's sums).
 #pragma once
 
 #include <cstdint>
@@ -27,7 +30,8 @@ constexpr int kRoBlockRows = 1 << 14;
 constexpr int kRoApplyWaves = 14;               // waves 0..13 apply, 14..15 load x
 constexpr int kRoLoadWaves = 2;
 constexpr int kRoWaveRows = (kRoBlockRows + kRoApplyWaves - 1) / kRoApplyWaves;   // 1171
-constexpr int kRoMaxWindows = 1 << 13;          // window index field
+constexpr int kRoMaxWindows = 1 << 12;          // window index field (header bits 0-11)
+constexpr uint32_t kRoDepBit = 1u << 12;
 
 struct RoHost {
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
