@@ -23,6 +23,9 @@
 #include "xband.h"
 #include "xband_dev.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace smamd {
 namespace {
 
@@ -30,7 +33,6 @@ constexpr int kRoThreads = 1024;
 constexpr int kRoBufs = 3;
 constexpr int kRoPieces = kRoWindow / 256;                       // 30
 constexpr int kRoPpl = (kRoPieces + kRoLoadWaves - 1) / kRoLoadWaves;   // 15
-constexpr int kRoAE = 3;                                          // entry pairs in flight
 constexpr int kRoTab = 4;                                         // table copies
 constexpr uint32_t kRoColMask = (1u << 13) - 1u;
 constexpr uint32_t kRoWinMask = (uint32_t)kRoMaxWindows - 1u;
@@ -38,6 +40,16 @@ constexpr int kRoOffShift = 13 + kCbIdBits;                       // 21
 static_assert(kRoApplyWaves + kRoLoadWaves == kRoThreads / 64, "roles fill the workgroup");
 static_assert(kRoPieces % kRoLoadWaves == 0, "whole pieces per loader");
 
+#ifdef SM_DEV
+// PROF (SM_RO_PROF=1, development): cycles per wave -- [0] prologue, [1] applying: waiting for
+// the loaders, [2] applying: the rest of the chunk loop, [3] epilogue; [4] loader: waiting for
+// the applying waves, [5] loader: DMA issue + landing; [6] pairs, [7] pairs applied in turn,
+// [8] applying waves | loader waves << 32.
+__device__ unsigned long long g_ro_prof[10];
+#endif
+
+// AE: entry pairs in flight per applying wave (3; development builds take SM_RO_AE=6).
+template <bool PROF, int AE>
 __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
     int32_t n_rows, int32_t n_cols, int32_t n_slabs, int32_t slab_cols, const int32_t *__restrict__ wave_start,
     const uint32_t *__restrict__ ent, uint64_t ent_bytes, const float *__restrict__ table, int32_t table_size,
@@ -50,6 +62,15 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
     __shared__ int32_t ldp[kRoLoadWaves];   // loader l: its pieces of windows < ldp[l] have landed
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    [[maybe_unused]] unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] unsigned long long tk = PROF ? clock64() : 0;
+    auto mark = [&](int k) {
+        if constexpr (PROF) {
+            const unsigned long long now = clock64();
+            ph[k] += now - tk;
+            tk = now;
+        }
+    };
     const int32_t t = blockIdx.x;
     const int32_t b = t / n_slabs, slab = t - b * n_slabs;
     const uint64_t old_started = handoff_begin(ctl + (int64_t)b * kCtlWords, n_slabs);
@@ -97,10 +118,10 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
     if (wid >= kRoApplyWaves) {
         for (int32_t q = 0; q < min(nq, 2); ++q) dma_win(q);
     }
-    uint32_t E[kRoAE][2];
+    uint32_t E[AE][2];
     if (wid < kRoApplyWaves) {
 #pragma unroll
-        for (int v = 0; v < kRoAE; ++v) {
+        for (int v = 0; v < AE; ++v) {
             E[v][0] = load_c(2 * v);
             E[v][1] = load_c(2 * v + 1);
         }
@@ -138,6 +159,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
     if (tid < kRoLoadWaves) ldp[tid] = 0;
     __syncthreads();
     const uint64_t snap = handoff_snapshot(ctl + (int64_t)b * kCtlWords, n_slabs);
+    mark(0);
 
     if (wid >= kRoApplyWaves) {
         // ---- loader ------------------------------------------------------------------
@@ -146,11 +168,13 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
             if (q >= 2) {
                 if (q >= kRoBufs) {   // buffer q % 3 held window q - 3: every applying wave past it
                     const int32_t need = q - 2;
+                    mark(5);
                     for (;;) {
                         const int32_t p = lane < kRoApplyWaves ? lds_ld(&prog[lane]) : need;
                         if (__ballot(p < need) == 0) break;
                         __builtin_amdgcn_s_sleep(1);
                     }
+                    mark(4);
                 }
                 dma_win(q);
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRoPpl) : "memory");   // window q - 1 landed
@@ -162,6 +186,8 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) lds_st(&ldp[ld], nq);
+        mark(5);
+        ph[8] = 1ull << 32;
     } else {
         // ---- applying wave -----------------------------------------------------------
         const int32_t wrow = wid * kRoWaveRows;   // the wave's first row in the block
@@ -177,10 +203,10 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
             return r;
         };
         const int32_t npair = (nch + 1) >> 1;
-        const int32_t npu = (npair + kRoAE - 1) / kRoAE * kRoAE;
-        for (int32_t p0 = 0; p0 < npu; p0 += kRoAE) {
+        const int32_t npu = (npair + AE - 1) / AE * AE;
+        for (int32_t p0 = 0; p0 < npu; p0 += AE) {
 #pragma unroll
-            for (int u = 0; u < kRoAE; ++u) {
+            for (int u = 0; u < AE; ++u) {
                 const int32_t pi = p0 + u;
                 if (pi < npair) {   // wave-uniform
                     uint32_t wd[2], qk[2], base[2], dep1 = 0;
@@ -197,10 +223,16 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                         done_q = (int32_t)qk[0];
                         if (lane == 0) lds_st(&prog[wid], done_q);
                     }
+                    mark(2);
                     while (ready <= (int32_t)qk[1]) {   // both loaders' pieces of window qk[1]
                         const int32_t a = lds_ld(&ldp[0]), bb = lds_ld(&ldp[1]);
                         ready = min(a, bb);
                         if (ready <= (int32_t)qk[1]) __builtin_amdgcn_s_sleep(1);
+                    }
+                    mark(1);
+                    if constexpr (PROF) {
+                        ph[6] += 1;
+                        ph[7] += dep1 ? 1 : 0;
                     }
                     __builtin_amdgcn_s_setprio(2);
                     // together (one pass) unless the second chunk reads a row the first writes:
@@ -245,12 +277,25 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                     }
                     __builtin_amdgcn_s_setprio(0);
                 }
-                E[u][0] = load_c(2 * (pi + kRoAE));
-                E[u][1] = load_c(2 * (pi + kRoAE) + 1);
+                E[u][0] = load_c(2 * (pi + AE));
+                E[u][1] = load_c(2 * (pi + AE) + 1);
             }
         }
         if (lane == 0) lds_st(&prog[wid], nq);   // every window read
+        mark(2);
+        ph[8] = 1;
     }
+    auto flush = [&]() {
+#ifdef SM_DEV
+        if constexpr (PROF) {
+            mark(3);
+            if (lane == 0) {
+                for (int k = 0; k < 8; ++k) atomicAdd(&g_ro_prof[k], ph[k]);
+                atomicAdd(&g_ro_prof[8], ph[8]);
+            }
+        }
+#endif
+    };
     __syncthreads();   // every wave done: the sums are final, the hand-off words live in xs
     if (n_slabs == 1) {
         const int32_t nv = y_vec ? (nr & ~3) : 0;
@@ -260,11 +305,13 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
             if (i < nv) *reinterpret_cast<float4 *>(y + r0 + i) = *reinterpret_cast<const float4 *>(&yacc[i]);
         }
         for (int32_t i = nv + tid; i < nr; i += kRoThreads) y[r0 + i] = yacc[i];
+        flush();
         return;
     }
     int32_t *s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
     slab_handoff_epoch<kRoThreads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0, nr, slab,
                                    n_slabs, y_vec, old_started, snap);
+    flush();
 }
 
 }  // namespace
@@ -277,10 +324,44 @@ hipError_t launch_spmv_ro(const XbandDev &d, int32_t n_rows, int32_t n_cols, con
     if (d.kind != kXbRo || !d.d_chunk_start || !d.d_word || !d.d_table || d.table_size < 0 ||
         d.table_size > (int32_t)kCbDummyId || d.block_rows > kRoBlockRows || (d.n_slabs > 1 && (!d.d_partials || !d.d_tickets)))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(spmv_ro_kernel, dim3((unsigned)((int64_t)d.n_blocks * d.n_slabs)), dim3(kRoThreads), 0, s,
-                       n_rows, n_cols, d.n_slabs, d.slab_bands, d.d_chunk_start, d.d_word,
-                       (uint64_t)d.n_chunks * 256u, d.d_table, d.table_size, x, y, d.d_partials, d.d_tickets,
-                       alpha, beta);
+#define SM_RO(P, A)                                                                                 \
+    hipLaunchKernelGGL((spmv_ro_kernel<P, A>), dim3((unsigned)((int64_t)d.n_blocks * d.n_slabs)), dim3(kRoThreads), 0, s, \
+                       n_rows, n_cols, d.n_slabs, d.slab_bands, d.d_chunk_start, d.d_word,             \
+                       (uint64_t)d.n_chunks * 256u, d.d_table, d.table_size, x, y, d.d_partials, d.d_tickets, \
+                       alpha, beta)
+#ifdef SM_DEV
+    static const bool prof = [] {
+        const char *e = dev_env("SM_RO_PROF");
+        return e && atoi(e) != 0;
+    }();
+    static const int ae = [] {
+        const char *e = dev_env("SM_RO_AE");
+        return e ? atoi(e) : 3;
+    }();
+    if (ae != 3 && ae != 6) return hipErrorInvalidValue;
+    if (prof) {
+        unsigned long long h[10] = {};
+        void *sym = nullptr;
+        if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_ro_prof)) != hipSuccess) return hipErrorInvalidValue;
+        (void)hipMemsetAsync(sym, 0, sizeof(h), s);
+        if (ae == 6) SM_RO(true, 6);
+        else SM_RO(true, 3);
+        (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const double wa = (double)(h[8] & 0xFFFFFFFFull), wl = (double)(h[8] >> 32);
+        fprintf(stderr, "ro prof (cycles per wave; %.0f applying + %.0f loader waves; %.1f pairs, %.1f in turn per "
+                "applying wave): applying: prologue %.0f loader wait %.0f chunks %.0f epilogue %.0f | loaders: "
+                "wait %.0f dma %.0f\n", wa, wl, h[6] / wa, h[7] / wa, h[0] / (wa + wl), h[1] / wa, h[2] / wa,
+                h[3] / (wa + wl), h[4] / wl, h[5] / wl);
+        return hipGetLastError();
+    }
+    if (ae == 6) {
+        SM_RO(false, 6);
+        return hipGetLastError();
+    }
+#endif
+    SM_RO(false, 3);
+#undef SM_RO
     return hipGetLastError();
 }
 
