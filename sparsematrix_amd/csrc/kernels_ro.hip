@@ -48,8 +48,11 @@ static_assert(kRoPieces % kRoLoadWaves == 0, "whole pieces per loader");
 __device__ unsigned long long g_ro_prof[10];
 #endif
 
-// AE: entry pairs in flight per applying wave (3; development builds take SM_RO_AE=6).
-template <bool PROF, int AE>
+constexpr int AE = 3;   // entry pairs in flight per applying wave (6 measured the same)
+
+// ABL (development ablations, SM_RO_ABLATE, results wrong): 1 the loaders issue no DMA, 2 no x
+// reads, 4 no sum reads or writes, 8 no apply at all, 16 no waits on the loaders.
+template <bool PROF, int ABL>
 __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
     int32_t n_rows, int32_t n_cols, int32_t n_slabs, int32_t slab_cols, const int32_t *__restrict__ wave_start,
     const uint32_t *__restrict__ ent, uint64_t ent_bytes, const float *__restrict__ table, int32_t table_size,
@@ -116,7 +119,8 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
         return __builtin_amdgcn_raw_buffer_load_b32(e_src, off, 0, kAuxNt);
     };
     if (wid >= kRoApplyWaves) {
-        for (int32_t q = 0; q < min(nq, 2); ++q) dma_win(q);
+        if constexpr (!(ABL & 1))
+            for (int32_t q = 0; q < min(nq, 2); ++q) dma_win(q);
     }
     uint32_t E[AE][2];
     if (wid < kRoApplyWaves) {
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                     }
                     mark(4);
                 }
-                dma_win(q);
+                if constexpr (!(ABL & 1)) dma_win(q);
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRoPpl) : "memory");   // window q - 1 landed
                 if (lane == 0) lds_st(&ldp[ld], q);
             } else if (q == 1) {
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                         if (lane == 0) lds_st(&prog[wid], done_q);
                     }
                     mark(2);
-                    while (ready <= (int32_t)qk[1]) {   // both loaders' pieces of window qk[1]
+                    while (!(ABL & 16) && ready <= (int32_t)qk[1]) {   // both loaders' pieces of window qk[1]
                         const int32_t a = lds_ld(&ldp[0]), bb = lds_ld(&ldp[1]);
                         ready = min(a, bb);
                         if (ready <= (int32_t)qk[1]) __builtin_amdgcn_s_sleep(1);
@@ -238,7 +242,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                     // together (one pass) unless the second chunk reads a row the first writes:
                     // then pass 0 applies the first alone and pass 1 the second
                     const int npass = dep1 ? 2 : 1;
-                    for (int ps = 0; ps < npass; ++ps) {
+                    for (int ps = 0; ps < npass && !(ABL & 8); ++ps) {
                     const uint64_t on[2] = {(!dep1 || ps == 0) ? ~1ull : 0ull, (!dep1 || ps == 1) ? ~1ull : 0ull};
                     float xv[2], tv[2], yv[2];
                     uint32_t rl[2];
@@ -249,9 +253,9 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
                         live[k] = __ballot(id != kCbDummyId) & on[k];
                         cont[k] = __ballot((int32_t)wd[k] < 0) & on[k];
                         rl[k] = base[k] + ((wd[k] >> kRoOffShift) & kCbOffMask);
-                        xv[k] = xs[qk[k] % kRoBufs][wd[k] & kRoColMask];
+                        xv[k] = (ABL & 2) ? 1.0f : xs[qk[k] % kRoBufs][wd[k] & kRoColMask];
                         tv[k] = tab[id * kRoTab + (lane & (kRoTab - 1))];
-                        yv[k] = yacc[min(rl[k], (uint32_t)(kRoBlockRows - 1))];
+                        yv[k] = (ABL & 4) ? 0.0f : yacc[min(rl[k], (uint32_t)(kRoBlockRows - 1))];
                     }
                     asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
                     float tm[2], acc[2];
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
                         const uint64_t last = live[k] & ~(cont[k] >> 1);
-                        if ((last >> lane) & 1) yacc[rl[k]] = acc[k];
+                        if (!(ABL & 4) && ((last >> lane) & 1)) yacc[rl[k]] = acc[k];
                     }
                     }
                     __builtin_amdgcn_s_setprio(0);
@@ -334,33 +338,44 @@ hipError_t launch_spmv_ro(const XbandDev &d, int32_t n_rows, int32_t n_cols, con
         const char *e = dev_env("SM_RO_PROF");
         return e && atoi(e) != 0;
     }();
-    static const int ae = [] {
-        const char *e = dev_env("SM_RO_AE");
-        return e ? atoi(e) : 3;
+    static const int abl = [] {
+        const char *e = dev_env("SM_RO_ABLATE");
+        return e ? atoi(e) : 0;
     }();
-    if (ae != 3 && ae != 6) return hipErrorInvalidValue;
+#define SM_RO_ABL(P)                                                                                \
+    switch (abl) {                                                                                  \
+    case 0: SM_RO(P, 0); break;                                                                     \
+    case 1: SM_RO(P, 1); break;                                                                     \
+    case 2: SM_RO(P, 2); break;                                                                     \
+    case 4: SM_RO(P, 4); break;                                                                     \
+    case 6: SM_RO(P, 6); break;                                                                     \
+    case 8: SM_RO(P, 8); break;                                                                     \
+    case 16: SM_RO(P, 16); break;                                                                   \
+    case 25: SM_RO(P, 25); break;                                                                   \
+    default: return hipErrorInvalidValue;                                                           \
+    }
     if (prof) {
         unsigned long long h[10] = {};
         void *sym = nullptr;
         if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_ro_prof)) != hipSuccess) return hipErrorInvalidValue;
         (void)hipMemsetAsync(sym, 0, sizeof(h), s);
-        if (ae == 6) SM_RO(true, 6);
-        else SM_RO(true, 3);
+        SM_RO_ABL(true)
         (void)hipMemcpyAsync(h, sym, sizeof(h), hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         const double wa = (double)(h[8] & 0xFFFFFFFFull), wl = (double)(h[8] >> 32);
-        fprintf(stderr, "ro prof (cycles per wave; %.0f applying + %.0f loader waves; %.1f pairs, %.1f in turn per "
+        fprintf(stderr, "ro prof abl %d (cycles per wave; %.0f applying + %.0f loader waves; %.1f pairs, %.1f in turn per "
                 "applying wave): applying: prologue %.0f loader wait %.0f chunks %.0f epilogue %.0f | loaders: "
-                "wait %.0f dma %.0f\n", wa, wl, h[6] / wa, h[7] / wa, h[0] / (wa + wl), h[1] / wa, h[2] / wa,
+                "wait %.0f dma %.0f\n", abl, wa, wl, h[6] / wa, h[7] / wa, h[0] / (wa + wl), h[1] / wa, h[2] / wa,
                 h[3] / (wa + wl), h[4] / wl, h[5] / wl);
         return hipGetLastError();
     }
-    if (ae == 6) {
-        SM_RO(false, 6);
+    if (abl != 0) {
+        SM_RO_ABL(false)
         return hipGetLastError();
     }
+#undef SM_RO_ABL
 #endif
-    SM_RO(false, 3);
+    SM_RO(false, 0);
 #undef SM_RO
     return hipGetLastError();
 }
