@@ -5,8 +5,8 @@
 // through three 30 KiB LDS windows by LDS-DMA, the <= 255-entry table scaled by alpha in
 // LDS (4 copies), the slab hand-off of xband_dev.h.  Roles:
 //   waves 0..13 apply: wave w owns the block's rows [w * 1171, (w + 1) * 1171) and walks its
-//     own chunk stream (ro.cpp) two chunks at a time, in window order -- together when their
-//     rows are disjoint, else (kRoDepBit on the second) the first and then the second;
+//     own chunk stream (ro.cpp) four chunks at a time, in window order, stage by stage (ro.h:
+//     a stage's chunks have disjoint rows, so they are applied together);
 //   waves 14..15 load: each issues half of every window's 30 1 KiB pieces.
 // No barrier between windows: a wave applies window q's chunks once both loaders have
 // published window q in LDS (ldp[] >= q + 1), and publishes prog[w] = q when it moves on to
@@ -48,7 +48,7 @@ static_assert(kRoPieces % kRoLoadWaves == 0, "whole pieces per loader");
 __device__ unsigned long long g_ro_prof[10];
 #endif
 
-constexpr int AE = 3;   // entry pairs in flight per applying wave (6 measured the same)
+constexpr int AE = 2;   // entry groups (kRoGroup chunks) in flight per applying wave
 
 // ABL (development ablations, SM_RO_ABLATE, results wrong): 1 the loaders issue no DMA, 2 no x
 // reads, 4 no sum reads or writes, 8 no apply at all, 16 no waits on the loaders.
@@ -122,13 +122,13 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
         if constexpr (!(ABL & 1))
             for (int32_t q = 0; q < min(nq, 2); ++q) dma_win(q);
     }
-    uint32_t E[AE][2];
+    constexpr int G = kRoGroup;
+    uint32_t E[AE][G];
     if (wid < kRoApplyWaves) {
 #pragma unroll
-        for (int v = 0; v < AE; ++v) {
-            E[v][0] = load_c(2 * v);
-            E[v][1] = load_c(2 * v + 1);
-        }
+        for (int v = 0; v < AE; ++v)
+#pragma unroll
+            for (int k = 0; k < G; ++k) E[v][k] = load_c(G * v + k);
     }
     {   // table: fl(table[id] * alpha), four copies, id 255 (dummies) and past the table 0
         const int id = tid >> 2;
@@ -167,29 +167,40 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
 
     if (wid >= kRoApplyWaves) {
         // ---- loader ------------------------------------------------------------------
+        // Issue the next window as soon as its buffer is free (every applying wave has moved
+        // past the window it held), else publish the oldest window in flight once it lands:
+        // a wave reading window p may so have p + 1 and p + 2 landed beside it.
         __builtin_amdgcn_s_setprio(3);
-        for (int32_t q = 0; q < nq; ++q) {
-            if (q >= 2) {
-                if (q >= kRoBufs) {   // buffer q % 3 held window q - 3: every applying wave past it
-                    const int32_t need = q - 2;
+        int32_t issued = min(nq, 2), landed = 0;
+        while (landed < nq) {
+            bool can = false;
+            if (issued < nq) {
+                if (issued < kRoBufs) {
+                    can = true;
+                } else {   // buffer issued % 3 held window issued - 3
+                    const int32_t need = issued - 2;
                     mark(5);
-                    for (;;) {
-                        const int32_t p = lane < kRoApplyWaves ? lds_ld(&prog[lane]) : need;
-                        if (__ballot(p < need) == 0) break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
+                    const int32_t p = lane < kRoApplyWaves ? lds_ld(&prog[lane]) : need;
+                    can = __ballot(p < need) == 0;
                     mark(4);
                 }
-                if constexpr (!(ABL & 1)) dma_win(q);
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRoPpl) : "memory");   // window q - 1 landed
-                if (lane == 0) lds_st(&ldp[ld], q);
-            } else if (q == 1) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRoPpl) : "memory");   // window 0 landed
-                if (lane == 0) lds_st(&ldp[ld], 1);
             }
+            if (can) {
+                if constexpr (!(ABL & 1)) dma_win(issued);
+                ++issued;
+                continue;
+            }
+            const int32_t out = issued - landed;   // windows in flight, oldest first
+            if (out == 0) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            if (out >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kRoPpl) : "memory");
+            else if (out == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRoPpl) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ++landed;
+            if (lane == 0) lds_st(&ldp[ld], landed);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) lds_st(&ldp[ld], nq);
         mark(5);
         ph[8] = 1ull << 32;
     } else {
@@ -206,83 +217,95 @@ __global__ __launch_bounds__(kRoThreads) void spmv_ro_kernel(
             asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(bb), "s"(m));
             return r;
         };
-        const int32_t npair = (nch + 1) >> 1;
-        const int32_t npu = (npair + AE - 1) / AE * AE;
-        for (int32_t p0 = 0; p0 < npu; p0 += AE) {
+        const int32_t ngrp = (nch + G - 1) / G;
+        const int32_t ngu = (ngrp + AE - 1) / AE * AE;
+        for (int32_t g0 = 0; g0 < ngu; g0 += AE) {
 #pragma unroll
             for (int u = 0; u < AE; ++u) {
-                const int32_t pi = p0 + u;
-                if (pi < npair) {   // wave-uniform
-                    uint32_t wd[2], qk[2], base[2], dep1 = 0;
+                const int32_t gi = g0 + u;
+                if (gi < ngrp) {   // wave-uniform
+                    uint32_t wd[G], qk[G], st[G], base[G];
+                    uint32_t qmax = 0, smax = 0;
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {
+                    for (int k = 0; k < G; ++k) {
                         wd[k] = E[u][k] ^ dmy;
                         const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)wd[k], 0);
                         qk[k] = h & kRoWinMask;
+                        st[k] = (h >> kRoStageShift) & 3u;
                         base[k] = (uint32_t)wrow + (((h >> kRoOffShift) & kCbOffMask) | ((h >> kCbContBit) << 10));
-                        if (k == 1) dep1 = h & kRoDepBit;
+                        if (k > 0 && G * gi + k >= nch) { qk[k] = qk[0]; st[k] = 0; }   // past the stream: a dummy
+                        qmax = max(qmax, qk[k]);
+                        smax = max(smax, st[k]);
                     }
-                    if (2 * pi + 1 >= nch) { qk[1] = qk[0]; dep1 = 0; }   // past the stream: a dummy chunk
-                    if ((int32_t)qk[0] > done_q) {   // moving on: windows < qk[0] are read in full
-                        done_q = (int32_t)qk[0];
-                        if (lane == 0) lds_st(&prog[wid], done_q);
-                    }
-                    mark(2);
-                    while (!(ABL & 16) && ready <= (int32_t)qk[1]) {   // both loaders' pieces of window qk[1]
-                        const int32_t a = lds_ld(&ldp[0]), bb = lds_ld(&ldp[1]);
-                        ready = min(a, bb);
-                        if (ready <= (int32_t)qk[1]) __builtin_amdgcn_s_sleep(1);
-                    }
-                    mark(1);
+                    // Stage by stage (each stage's chunks have disjoint rows), all windows of the
+                    // group landed first -- unless the group spans more windows than the ring
+                    // holds ahead of its first (the loaders refill window q only once every wave
+                    // has moved to q - 2): then chunk by chunk, publishing as it goes.
+                    const bool serial = qmax > qk[0] + 2;
+                    const int npass = serial ? G : (int)smax + 1;
                     if constexpr (PROF) {
                         ph[6] += 1;
-                        ph[7] += dep1 ? 1 : 0;
+                        ph[7] += (unsigned long long)(npass - 1);
                     }
-                    __builtin_amdgcn_s_setprio(2);
-                    // together (one pass) unless the second chunk reads a row the first writes:
-                    // then pass 0 applies the first alone and pass 1 the second
-                    const int npass = dep1 ? 2 : 1;
-                    for (int ps = 0; ps < npass && !(ABL & 8); ++ps) {
-                    const uint64_t on[2] = {(!dep1 || ps == 0) ? ~1ull : 0ull, (!dep1 || ps == 1) ? ~1ull : 0ull};
-                    float xv[2], tv[2], yv[2];
-                    uint32_t rl[2];
-                    uint64_t live[2], cont[2];
+                    for (int ps = 0; ps < npass; ++ps) {
+                        uint32_t qps = qk[0];   // qk[ps], without a dynamically indexed array
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const uint32_t id = (wd[k] >> 13) & kCbDummyId;
-                        live[k] = __ballot(id != kCbDummyId) & on[k];
-                        cont[k] = __ballot((int32_t)wd[k] < 0) & on[k];
-                        rl[k] = base[k] + ((wd[k] >> kRoOffShift) & kCbOffMask);
-                        xv[k] = (ABL & 2) ? 1.0f : xs[qk[k] % kRoBufs][wd[k] & kRoColMask];
-                        tv[k] = tab[id * kRoTab + (lane & (kRoTab - 1))];
-                        yv[k] = (ABL & 4) ? 0.0f : yacc[min(rl[k], (uint32_t)(kRoBlockRows - 1))];
-                    }
-                    asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(yv[0]), "+v"(yv[1]), "+v"(tv[0]), "+v"(tv[1]));
-                    float tm[2], acc[2];
-                    uint64_t R[2];
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        tm[k] = __fmul_rn(xv[k], tv[k]);
-                        acc[k] = __fadd_rn(yv[k], tm[k]);
-                        R[k] = cont[k] & ~(cont[k] << 1);
-                    }
-                    while ((R[0] | R[1]) != 0) {
-#pragma unroll
-                        for (int k = 0; k < 2; ++k) {
-                            acc[k] = sel(R[k], acc[k], __fadd_rn(shr1(acc[k]), tm[k]));
-                            R[k] = cont[k] & (R[k] << 1);
+                        for (int k = 1; k < G; ++k) qps = k == ps ? qk[k] : qps;
+                        const uint32_t qlo = serial ? qps : qk[0], qhi = serial ? qps : qmax;
+                        if ((int32_t)qlo > done_q) {   // moving on: windows < qlo are read in full
+                            done_q = (int32_t)qlo;
+                            if (lane == 0) lds_st(&prog[wid], done_q);
                         }
-                    }
+                        mark(2);
+                        while (!(ABL & 16) && ready <= (int32_t)qhi) {   // both loaders' pieces of window qhi
+                            const int32_t a = lds_ld(&ldp[0]), bb = lds_ld(&ldp[1]);
+                            ready = min(a, bb);
+                            if (ready <= (int32_t)qhi) __builtin_amdgcn_s_sleep(1);
+                        }
+                        mark(1);
+                        if constexpr (ABL & 8) continue;
+                        __builtin_amdgcn_s_setprio(2);
+                        float xv[G], tv[G], yv[G];
+                        uint32_t rl[G];
+                        uint64_t live[G], cont[G];
 #pragma unroll
-                    for (int k = 0; k < 2; ++k) {   // the segment's last lane writes its row
-                        const uint64_t last = live[k] & ~(cont[k] >> 1);
-                        if (!(ABL & 4) && ((last >> lane) & 1)) yacc[rl[k]] = acc[k];
+                        for (int k = 0; k < G; ++k) {
+                            const uint64_t on = (serial ? k == ps : st[k] == (uint32_t)ps) ? ~1ull : 0ull;
+                            const uint32_t id = (wd[k] >> 13) & kCbDummyId;
+                            live[k] = __ballot(id != kCbDummyId) & on;
+                            cont[k] = __ballot((int32_t)wd[k] < 0) & on;
+                            rl[k] = base[k] + ((wd[k] >> kRoOffShift) & kCbOffMask);
+                            xv[k] = (ABL & 2) ? 1.0f : xs[qk[k] % kRoBufs][wd[k] & kRoColMask];
+                            tv[k] = tab[id * kRoTab + (lane & (kRoTab - 1))];
+                            yv[k] = (ABL & 4) ? 0.0f : yacc[min(rl[k], (uint32_t)(kRoBlockRows - 1))];
+                        }
+                        asm volatile("" : "+v"(xv[0]), "+v"(xv[1]), "+v"(xv[2]), "+v"(xv[3]), "+v"(yv[0]), "+v"(yv[1]),
+                                     "+v"(yv[2]), "+v"(yv[3]), "+v"(tv[0]), "+v"(tv[1]), "+v"(tv[2]), "+v"(tv[3]));
+                        float tm[G], acc[G];
+                        uint64_t R[G];
+#pragma unroll
+                        for (int k = 0; k < G; ++k) {
+                            tm[k] = __fmul_rn(xv[k], tv[k]);
+                            acc[k] = __fadd_rn(yv[k], tm[k]);
+                            R[k] = cont[k] & ~(cont[k] << 1);
+                        }
+                        while ((R[0] | R[1] | R[2] | R[3]) != 0) {
+#pragma unroll
+                            for (int k = 0; k < G; ++k) {
+                                acc[k] = sel(R[k], acc[k], __fadd_rn(shr1(acc[k]), tm[k]));
+                                R[k] = cont[k] & (R[k] << 1);
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < G; ++k) {   // the segment's last lane writes its row
+                            const uint64_t last = live[k] & ~(cont[k] >> 1);
+                            if (!(ABL & 4) && ((last >> lane) & 1)) yacc[rl[k]] = acc[k];
+                        }
+                        __builtin_amdgcn_s_setprio(0);
                     }
-                    }
-                    __builtin_amdgcn_s_setprio(0);
                 }
-                E[u][0] = load_c(2 * (pi + AE));
-                E[u][1] = load_c(2 * (pi + AE) + 1);
+#pragma unroll
+                for (int k = 0; k < G; ++k) E[u][k] = load_c(G * (gi + AE) + k);
             }
         }
         if (lane == 0) lds_st(&prog[wid], nq);   // every window read

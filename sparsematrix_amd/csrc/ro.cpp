@@ -37,16 +37,19 @@ void build_tile(const int32_t *rp, const int32_t *col, const uint8_t *ids, int64
     if (nq > kRoMaxWindows) { out.ok = false; return; }
     out.wave_chunks.assign(kRoApplyWaves, 0);
     const uint32_t dmy = kRoGeom.cb_dummy_word(), cmask = (1u << kRoGeom.cb_col) - 1u;
+    (void)cmask;
     const int osh = kRoGeom.cb_off_shift();
     const int32_t span = kRoGeom.cb_row_span();   // 1024
     std::vector<int32_t> cur, end;
     std::vector<B2Seg> segs;
     std::vector<std::vector<B2Seg>> cs;
-    std::vector<int32_t> prev_rows, rows;   // rows of the wave's previous chunk / this one (sorted)
+    std::vector<int32_t> rows;
+    std::vector<std::vector<int32_t>> grp_rows(kRoGroup);   // rows (sorted) of the group's chunks so far
+    int grp_stage[kRoGroup] = {};
     for (int w = 0; w < kRoApplyWaves; w++) {
         const int64_t wr0 = r0 + (int64_t)w * kRoWaveRows, wr1 = std::min<int64_t>(r1, wr0 + kRoWaveRows);
         if (wr0 >= wr1) continue;
-        prev_rows.clear();
+        int32_t idx = 0;   // position in the wave's stream
         const int64_t nr = wr1 - wr0;
         cur.assign((size_t)nr, 0);
         end.assign((size_t)nr, 0);
@@ -94,16 +97,23 @@ void build_tile(const int32_t *rp, const int32_t *col, const uint8_t *ids, int64
                 const size_t at = out.ent.size();
                 out.ent.resize(at + 64, 0u);
                 b2_emit_chunk(out.ent.data() + at, 0, cs[(size_t)c], col, nullptr, ids, (int32_t)clo, kRoGeom);
-                // header: window index | dep | base row relative to the wave's first row (11 bits)
+                // header: window index | stage | base row relative to the wave's first row (11 bits)
                 const uint32_t brel = (uint32_t)(cs[(size_t)c].front().rl - (int32_t)(wr0 - r0));
                 rows.clear();
                 for (const B2Seg &g : cs[(size_t)c]) rows.push_back(g.rl);
                 std::sort(rows.begin(), rows.end());
-                bool dep = false;
-                for (int32_t r : rows) dep = dep || std::binary_search(prev_rows.begin(), prev_rows.end(), r);
-                prev_rows.swap(rows);
-                const uint32_t h = ((uint32_t)q & (cmask >> 1)) | (dep ? kRoDepBit : 0u) | dmy | ((brel & 1023u) << osh) |
-                                   ((brel >> 10) << kCbContBit);
+                const int gi = idx % kRoGroup;
+                int stage = 0;
+                for (int j = 0; j < gi; j++) {
+                    bool share = false;
+                    for (int32_t r : rows) share = share || std::binary_search(grp_rows[(size_t)j].begin(), grp_rows[(size_t)j].end(), r);
+                    if (share) stage = std::max(stage, grp_stage[j] + 1);
+                }
+                grp_rows[(size_t)gi].swap(rows);
+                grp_stage[gi] = stage;
+                idx++;
+                const uint32_t h = ((uint32_t)q & (uint32_t)(kRoMaxWindows - 1)) | ((uint32_t)stage << kRoStageShift) | dmy |
+                                   ((brel & 1023u) << osh) | ((brel >> 10) << kCbContBit);
                 out.ent[at] = h ^ dmy;
             }
             out.wave_chunks[(size_t)w] += nc;

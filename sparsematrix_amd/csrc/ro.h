@@ -13,11 +13,13 @@
 //
 // Entry word (stored XOR kCbDummyWord, zero = dummy): column - window start (13 bits) |
 // codebook id (8) | row - chunk base (10) | continuation (1), as cband.  Header (lane 0):
-// id 255; column field = the window index (bits 0-11) | kRoDepBit (the chunk shares a row
-// with the previous chunk of the wave's stream: a row cut in 63-term pieces, or a row with
-// terms in both windows); row field + continuation bit = the chunk's base row relative to
-// the wave's first row (11 bits).  The kernel applies two consecutive chunks together unless
-// the second carries kRoDepBit; then in turn (the second reads the first's sums).
+// id 255; column field = the window index (bits 0-10) | the chunk's stage (bits 11-12); row
+// field + continuation bit = the chunk's base row relative to the wave's first row (11 bits).
+// The kernel applies a wave's chunks in groups of kRoGroup (aligned in the wave's stream).
+// Stage: 0 unless the chunk shares a row with an earlier chunk of its group (a row cut in
+// 63-term pieces, or a row with terms in two windows); then 1 + the highest stage of those.
+// Chunks of one stage in a group have disjoint rows and a row's chunks ascend in stage, so the
+// kernel applies a group stage by stage, each stage's chunks together.
 #pragma once
 
 #include <cstdint>
@@ -30,8 +32,9 @@ constexpr int kRoBlockRows = 1 << 14;
 constexpr int kRoApplyWaves = 14;               // waves 0..13 apply, 14..15 load x
 constexpr int kRoLoadWaves = 2;
 constexpr int kRoWaveRows = (kRoBlockRows + kRoApplyWaves - 1) / kRoApplyWaves;   // 1171
-constexpr int kRoMaxWindows = 1 << 12;          // window index field (header bits 0-11)
-constexpr uint32_t kRoDepBit = 1u << 12;
+constexpr int kRoMaxWindows = 1 << 11;          // window index field (header bits 0-10)
+constexpr int kRoStageShift = 11;               // stage field (header bits 11-12)
+constexpr int kRoGroup = 4;                     // chunks a wave applies together
 
 struct RoHost {
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;

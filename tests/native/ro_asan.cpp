@@ -35,30 +35,34 @@ static int check(const std::vector<int32_t> &rp, const std::vector<int32_t> &col
                 const uint32_t *e = &h.ent[(size_t)c * 64];
                 const uint32_t hd = e[0] ^ dmy;
                 if (((hd >> 13) & kCbDummyId) != kCbDummyId) { printf("FAIL header id\n"); return 1; }
-                const int32_t q = (int32_t)(hd & 4095u);
-                const bool dep = (hd & kRoDepBit) != 0;
+                const int32_t q = (int32_t)(hd & (uint32_t)(kRoMaxWindows - 1));
+                const int32_t stage = (int32_t)((hd >> kRoStageShift) & 3u);
                 const int32_t brel = (int32_t)(((hd >> 21) & kCbOffMask) | ((hd >> 31) << 10));
                 if (q < prev_q) { printf("FAIL window order\n"); return 1; }
                 prev_q = q;
                 const int64_t clo = c0 + (int64_t)q * kRoWindow;
-                // the dep flag: set exactly when this chunk shares a row with the previous one of
-                // the wave's stream (the kernel then applies them in turn, else together)
-                if (c > cs) {
-                    const uint32_t ph = h.ent[(size_t)(c - 1) * 64] ^ dmy;
-                    const int32_t pb = (int32_t)(((ph >> 21) & kCbOffMask) | ((ph >> 31) << 10));
-                    std::vector<int32_t> prow;
+                // the stage: 1 + the highest stage of the earlier chunks of its group (kRoGroup
+                // aligned in the wave's stream) it shares a row with, else 0
+                {
+                    const int32_t gi = (c - cs) % kRoGroup;
+                    std::vector<int32_t> mine;
                     for (int l = 1; l < 64; l++) {
-                        const uint32_t wp = h.ent[(size_t)(c - 1) * 64 + l] ^ dmy;
-                        if (((wp >> 13) & kCbDummyId) != kCbDummyId) prow.push_back(pb + (int32_t)((wp >> 21) & kCbOffMask));
-                    }
-                    bool share = false;
-                    for (int l = 1; l < 64 && !share; l++) {
                         const uint32_t wc = e[l] ^ dmy;
-                        if (((wc >> 13) & kCbDummyId) == kCbDummyId) continue;
-                        const int32_t r = brel + (int32_t)((wc >> 21) & kCbOffMask);
-                        share = std::count(prow.begin(), prow.end(), r) > 0;
+                        if (((wc >> 13) & kCbDummyId) != kCbDummyId) mine.push_back(brel + (int32_t)((wc >> 21) & kCbOffMask));
                     }
-                    if (share != dep) { printf("FAIL dep flag\n"); return 1; }
+                    int32_t want = 0;
+                    for (int32_t j = c - gi; j < c; j++) {
+                        const uint32_t ph = h.ent[(size_t)j * 64] ^ dmy;
+                        const int32_t pb = (int32_t)(((ph >> 21) & kCbOffMask) | ((ph >> 31) << 10));
+                        bool share = false;
+                        for (int l = 1; l < 64 && !share; l++) {
+                            const uint32_t wp = h.ent[(size_t)j * 64 + l] ^ dmy;
+                            if (((wp >> 13) & kCbDummyId) == kCbDummyId) continue;
+                            share = std::count(mine.begin(), mine.end(), pb + (int32_t)((wp >> 21) & kCbOffMask)) > 0;
+                        }
+                        if (share) want = std::max(want, (int32_t)((ph >> kRoStageShift) & 3u) + 1);
+                    }
+                    if (want != stage) { printf("FAIL stage\n"); return 1; }
                 }
                 int32_t prev_row = -1;
                 std::vector<int32_t> seen;
