@@ -104,7 +104,7 @@ def available_cores() -> dict:
     return {"use": use, "affinity": aff, "cgroup_quota": quota, "nproc": os.cpu_count()}
 
 
-LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband", 6: "gcb", 7: "ro"}
+LAYOUTS = {0: "stream", 1: "exact", 2: "blocked", 3: "gather", 4: "band2", 5: "cband", 6: "gcb"}
 KERNELS = {"stream": "spmv_stream_kernel",
            "sell": "spmv_sell_kernel / spmv_csell_kernel (sorted sliced-ELL)",
            "exact": "spmv_xband_kernel (exact band layout)",
@@ -115,9 +115,7 @@ KERNELS = {"stream": "spmv_stream_kernel",
                     "by a loader wave's LDS-DMA, distributed slab combine)",
            "ccsell": "spmv_ccsell_kernel (column-chunked sorted sliced-ELL)",
            "gcb": "spmv_gcb_kernel (gathered chunk bands: 2016-term bands, x gathered, rows' sums in LDS)",
-           "sweep": "spmv_sweep_kernel (column-swept 256-row blocks, one wavefront each)",
-           "ro": "spmv_ro_kernel (row-owner codebook bands: 14 applying waves own rows, 2 loader waves "
-                 "stream x by LDS-DMA, LDS progress counters instead of per-band barriers)"}
+           "sweep": "spmv_sweep_kernel (column-swept 256-row blocks, one wavefront each)"}
 
 
 def layout_of(info: dict) -> str:
@@ -194,7 +192,7 @@ def main():
     ap.add_argument("--layout", default="auto",
                     help="A/B: force the matrix layout (sm_build_opts.layout name, e.g. gcb, gather)")
     ap.add_argument("--band-tall", type=int, default=0,
-                    help="A/B: sm_build_opts.band_tall (1 tall, 2 half2, 4 dma3, 6 wide, 7 dma3 tall, 8 dmaw, 9 dmaw4, 10 ro) for the config-2 matrices")
+                    help="A/B: sm_build_opts.band_tall (0/4 dma3, 6 wide) for the config-2 matrices")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-spmm", action="store_true")

@@ -120,8 +120,7 @@ typedef struct sm_info {
     int32_t has_xband;          /* column-band layout: 0 none, 1 exact (bit-identical),
                                    2 blocked, 3 gather, 4 band2 (balanced bands),
                                    5 cband (balanced bands, codebook words),
-                                   6 gcb (gathered chunk bands), 7 ro (row-owner
-                                   codebook bands, band_tall = 10);
+                                   6 gcb (gathered chunk bands);
                                    2-6 sum each column slab in the reference's
                                    order and add the slab sums in slab order     */
     int32_t xband_blocks, xband_bands;
@@ -221,11 +220,10 @@ typedef struct sm_build_opts {
     int32_t struct_size;       /* sizeof(sm_build_opts) as the caller compiled it      */
     int32_t layout;            /* sm_layout                                            */
     int32_t band_slabs;        /* balanced bands: column slabs per row block, 0 = auto  */
-    int32_t band_tall;         /* balanced bands: 1 = tall tiles (32K rows), 2 = half2
-                                  tiles (8K rows, 15872-column windows; codebook only),
-                                  4 = dma3 (a loader wave stages x by LDS-DMA into three
-                                  7680-column buffers; the default), 6 = wide, 7 = dma3
-                                  tall (32K rows, 2560-column buffers; codebook only)   */
+    int32_t band_tall;         /* balanced-band geometry: 0 or 4 = dma3 (a loader wave
+                                  stages x by LDS-DMA into three 7680-column buffers; the
+                                  default), 6 = wide (8192-column windows staged by every
+                                  wave); other values are SM_ERR_INVALID_ARG            */
     int32_t gather_band_log2;  /* gather bands: 13, 14 or 15 (log2 columns), 0 = auto  */
     int32_t sell;              /* sorted sliced-ELL: -1 auto (built when no band layout), 0 never */
     int32_t sell_codebook;     /* sell slots as column|id words: -1 auto, 0 never      */

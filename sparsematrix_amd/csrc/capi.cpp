@@ -21,7 +21,6 @@
 #include "sm_internal.h"
 #include "sell.h"
 #include "xband.h"
-#include "ro.h"
 
 using namespace smamd;
 
@@ -222,6 +221,8 @@ sm_status check_opts(const sm_build_opts *o) {
     if (r.layout < SM_LAYOUT_AUTO || r.layout > SM_LAYOUT_GCB)
         return fail(SM_ERR_INVALID_ARG, "unknown layout %d", r.layout);
     if (r.band_slabs < 0 || r.band_slabs > 16) return fail(SM_ERR_INVALID_ARG, "band_slabs not in [0, 16]");
+    if (r.band_tall != 0 && r.band_tall != 4 && r.band_tall != 6)
+        return fail(SM_ERR_INVALID_ARG, "band_tall must be 0 (dma3), 4 (dma3) or 6 (wide)");
     if (r.gather_band_log2 != 0 && (r.gather_band_log2 < 13 || r.gather_band_log2 > 15))
         return fail(SM_ERR_INVALID_ARG, "gather_band_log2 must be 0 or 13..15");
     if (r.tile_nnz != 0 && r.tile_nnz != 1024 && r.tile_nnz != 2048 && r.tile_nnz != 4096 &&
@@ -326,27 +327,15 @@ bool want_xband(const sm_matrix *m) {
 // values take <= 255 distinct bit patterns, else (or kind band2) 8-byte entries.
 // Builds into `d` the balanced bands of an n_rows x n_cols CSR (the matrix's own, or
 // the hot column prefix of a relabeled graph); `forced`: keep mostly-padding bands.
-// Geometry (sm_build_opts.band_tall): 0 = the default (dma3, both encodings), 1 = tall,
-// 2 = half2, 4 = dma3, 6 = wide, 7 = dma3 tall (codebook words; config 2: 41.5 vs 33.6 us,
-// DESIGN.md §3.4b); development
-// builds also take 3 = wide3 for codebook values (three chunks per wave, 12160-column
-// windows, one table copy; config 2: 38.5 vs 37.2 us wide -- the table's bank conflicts
-// cost what the third fewer bands save: 36.1 vs 36.2 us with the lookup ablated).
+// Geometry (sm_build_opts.band_tall): 0 = the default (dma3, both encodings: a loader wave
+// stages x -- config 2 34.0-34.6 vs 36.9-37.1 us for the wide geometry with codebook words,
+// 37.9-38.0 vs 38.6-38.7 with 8-byte entries), 4 = dma3, 6 = wide.  dma3
+// bands that would be < 70 % full fall back to wide.
 static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
                              int32_t geo_opt, int32_t slabs, bool forced, int32_t slab0_permille = 1000) {
-    const bool tall = geo_opt == 1;
-    const bool half2 = geo_opt == 2 && kind == kXbCband;
-    // Both encodings default to dma3 (a loader wave stages x: config 2 34.0-34.6 vs 36.9-37.1
-    // us for the wide geometry with codebook words, 37.9-38.0 vs 38.6-38.7 with 8-byte
-    // entries); band_tall = 6 keeps the wide one.
-    if (geo_opt == 0) geo_opt = 4;   // dma3 for codebook words and 8-byte entries alike
-    const bool dma3 = geo_opt == 4 || ((geo_opt == 5 || geo_opt == 7 || geo_opt == 8 || geo_opt == 9) && kind == kXbCband);
-    const B2Geom geom = half2 ? kB2Half2Cb
-                      : dma3 ? (geo_opt == 5 ? kB2Dma3tCb : geo_opt == 7 ? kB2Dma3TallCb : geo_opt == 8 ? kB2DmawCb : geo_opt == 9 ? kB2Dmaw4Cb
-                                : kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2)
-                      : !tall ? kB2Wide
-                      : kind == kXbCband ? kB2TallCb : kB2TallB2;
+    const bool dma3 = geo_opt != 6;
+    const B2Geom geom = dma3 ? (kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
     const int64_t nblk = (n_rows + br - 1) / br;
     int32_t want = (int32_t)std::max<int64_t>(
@@ -356,18 +345,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     std::vector<uint8_t> ids;
     const bool cb = kind == kXbCband && codebook_ids(val, nnz, table, ids);
     Band2Host bh;
-#ifdef SM_DEV
-    const bool wide3 = cb && geo_opt == 3;
-#else
-    const bool wide3 = false;
-#endif
-    B2Geom g = tall ? (cb ? kB2TallCb : kB2TallB2) : wide3 ? kB2Wide3Cb : kB2Wide;
-    if (geo_opt == 2 || geo_opt == 4 || geo_opt == 5 || geo_opt == 7 || geo_opt == 8 || geo_opt == 9) {   // half2 / dma3* / dmaw: codebook words
-        if (cb) g = geo_opt == 2 ? kB2Half2Cb : geo_opt == 4 ? kB2Dma3Cb : geo_opt == 5 ? kB2Dma3tCb
-                    : geo_opt == 8 ? kB2DmawCb : geo_opt == 9 ? kB2Dmaw4Cb : kB2Dma3TallCb;
-        else if (geo_opt == 4) g = kB2Dma3B2;  // 8-byte entries, dma3
-        else return SM_OK;                    // a codebook-only geometry was asked for
-    }
+    B2Geom g = dma3 ? (cb ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
     // Bands are fixed slots of g.chunks() * 64 entries: where a slab's density leaves
     // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
     // bytes than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
@@ -378,7 +356,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
                (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
     };
     bool ok = fits(g);
-    if (!ok && (g.cpw == 3 || g.nch != 0)) {   // wide3 / dma3* did not fit: wide
+    if (!ok && g.nch != 0) {   // dma3 did not fit: wide
         g = kB2Wide;
         ok = fits(g);
     }
@@ -418,63 +396,14 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
     d.slab0_cols = bh.slab0_cols;
-    d.chunks_per_wave = g.cpw;
     d.n_chunks = bh.n_bands * g.chunks();
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
     return SM_OK;
 }
 
-// Row-owner codebook bands (ro.h, kernels_ro.hip; band_tall = 10): applying waves own rows,
-// no barrier between windows.
-static sm_status upload_ro(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
-    std::vector<float> table;
-    std::vector<uint8_t> ids;
-    if (!codebook_ids(val, m->nnz, table, ids)) return SM_OK;
-    const int64_t nblk = (m->n_rows + kRoBlockRows - 1) / kRoBlockRows;
-    int32_t slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
-    if (m->opts.band_slabs > 0) slabs = m->opts.band_slabs;
-    RoHost h;
-    if (!ro_build(rp, col, ids.data(), m->n_rows, m->n_cols, slabs, h)) return SM_OK;
-    std::vector<uint8_t>().swap(ids);
-    XbandDev &d = m->plan.xb;
-    const int64_t ntile = (int64_t)h.n_blocks * h.n_slabs;
-    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile * kRoApplyWaves + 1, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, h.n_chunks * 64), m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_table, 256, m->device_bytes));
-    SM_TRY_HIP(hipMemset(d.d_table, 0, 256 * sizeof(float)));
-    if (!table.empty())
-        SM_TRY_HIP(hipMemcpy(d.d_table, table.data(), table.size() * 4, hipMemcpyHostToDevice));
-    d.table_size = (int32_t)table.size();
-    if (h.n_slabs > 1) {
-        const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;
-        SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(h.n_slabs - 1) * ps, m->device_bytes));
-        SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)h.n_blocks, m->device_bytes));
-        SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)h.n_blocks * 4 * sizeof(int32_t)));
-    }
-    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, h.wave_start.data(), h.wave_start.size() * 4, hipMemcpyHostToDevice));
-    if (h.n_chunks > 0)
-        SM_TRY_HIP(hipMemcpy(d.d_word, h.ent.data(), (size_t)h.n_chunks * 256, hipMemcpyHostToDevice));
-    d.kind = kXbRo;
-    d.threads = 1024;
-    d.block_rows = h.block_rows;
-    d.band_cols = kRoWindow;
-    d.n_bands = (int32_t)std::min<int64_t>(h.n_chunks, INT32_MAX);   // chunks
-    d.n_slabs = h.n_slabs;
-    d.slab_bands = h.slab_cols;
-    d.slab0_cols = h.slab_cols;
-    d.n_chunks = h.n_chunks;
-    d.max_chunks_per_band = h.max_chunks_per_wave;
-    d.n_blocks = h.n_blocks;
-    return SM_OK;
-}
-
 static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *col,
                               const float *val, XbKind kind) {
-    if (kind == kXbCband && m->opts.band_tall == 10) {
-        const sm_status st = upload_ro(m, rp, col, val);
-        if (st != SM_OK || m->plan.xb.n_blocks > 0) return st;
-    }
     // Geometry: band_tall (xband.h B2Geom, build_band2).
     // Slab 0's tile loads and scales y (64 KiB per 16K-row block from HBM) before its first
     // band: on config 2 its band loop ended 1.5-2.3 us after the other slabs' (per-tile
@@ -1517,7 +1446,7 @@ sm_status sm_get_info(const sm_matrix *m, sm_info *info) {
 sm_status sm_debug_seed_handoff(sm_matrix *m, uint64_t started) {
     if (!m) return fail(SM_ERR_INVALID_ARG, "null matrix");
     const XbandDev &xb = m->plan.xb;
-    if (xb.n_blocks <= 0 || (xb.kind != kXbBand2 && xb.kind != kXbCband && xb.kind != kXbRo) || xb.n_slabs < 2 || !xb.d_tickets)
+    if (xb.n_blocks <= 0 || (xb.kind != kXbBand2 && xb.kind != kXbCband) || xb.n_slabs < 2 || !xb.d_tickets)
         return fail(SM_ERR_NOT_SUPPORTED, "no multi-slab band2/cband layout");
     if (started % (uint64_t)xb.n_slabs != 0)
         return fail(SM_ERR_NOT_SUPPORTED, "started must be a multiple of the slab count");
@@ -1555,8 +1484,7 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     info->xband_block_rows = m->plan.xb.block_rows;
     info->xband_slab_cols =
         m->plan.xb.n_blocks == 0 ? 0
-        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb ||
-                  m->plan.xb.kind == kXbRo
+        : m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband || m->plan.xb.kind == kXbGcb
             ? m->plan.xb.slab_bands   // band2 / cband / gcb keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->xband_slab0_cols = m->plan.xb.slab0_cols > 0 ? m->plan.xb.slab0_cols : info->xband_slab_cols;
@@ -1758,8 +1686,6 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         if (m->plan.xb.n_blocks > 0 && ((uintptr_t)x % 16) == 0) {
             e = m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband
                     ? launch_spmv_band2(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
-                : m->plan.xb.kind == kXbRo
-                    ? launch_spmv_ro(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                 : m->plan.xb.kind == kXbGcb
                     ? launch_spmv_gcb(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s)
                     : launch_spmv_xband(m->plan.xb, n, (int32_t)m->n_cols, x, y, alpha, beta, s);

@@ -75,7 +75,6 @@ struct XbandDev {
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int32_t n_slabs = 1, slab_bands = 0;   // tiles = n_blocks * n_slabs
     int32_t slab0_cols = 0;           // band2 / cband: columns of slab 0 (others: slab_bands)
-    int32_t chunks_per_wave = 2;      // band2 / cband: the geometry's chunks per applying wave
     int64_t n_chunks = 0;
     int64_t max_chunks_per_band = 0;
     int32_t *d_chunk_start = nullptr;
@@ -231,9 +230,6 @@ hipError_t launch_spmv_gcb(const XbandDev &xb, int32_t n_rows, int32_t n_cols, c
                            float alpha, float beta, hipStream_t s);
 hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x,
                              float *y, float alpha, float beta, hipStream_t s);
-// Row-owner codebook bands (ro.h, kernels_ro.hip): xb.kind == kXbRo.
-hipError_t launch_spmv_ro(const XbandDev &xb, int32_t n_rows, int32_t n_cols, const float *x, float *y,
-                          float alpha, float beta, hipStream_t s);
 // xp[rank[c]] = x[c], c < n (rank: original column -> new column).
 hipError_t launch_x_relabel(int64_t n, const int32_t *rank, const float *x, float *xp,
                             hipStream_t s);

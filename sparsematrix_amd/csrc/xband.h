@@ -28,8 +28,7 @@ constexpr XbBits xb_bits(int band_cols_log2, int block_rows_log2) {
 //  gather  -- blocked tiles, but x is not staged: a band's terms are listed in
 //             column order so the x gathers of one wave-instruction hit a few cache
 //             lines; LDS holds only the accumulators (measured slower, kept for A/B).
-enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5, kXbGcb = 6,
-                        kXbRo = 7 };
+enum XbKind : int32_t { kXbExact = 1, kXbBlocked = 2, kXbGather = 3, kXbBand2 = 4, kXbCband = 5, kXbGcb = 6 };
 constexpr int kXbExactBandLog2 = 14, kXbExactRowsLog2 = 12;
 constexpr int kXbBlockedBandLog2 = 13, kXbBlockedRowsLog2 = 14;
 constexpr int kXbGatherBandLog2 = 13, kXbGatherRowsLog2 = 14;
@@ -102,17 +101,13 @@ constexpr int kCbChunkTerms = 63;        // lane 0 is the header
 constexpr int kCbRowSpan = 1 << kCbOffBits;
 static_assert(kB2Window <= (1 << kCbColBits), "window column fits the column field");
 
-// Tile geometry.  wide: 16K-row blocks, 8192-column windows (the tile's block sums
-// in 64 KiB of LDS, two 32 KiB x windows); tall: 32K-row blocks (128 KiB of sums)
-// and 4096-column windows (cband: 3840, its table takes 1 KiB) -- half the x per
-// term of a tile, twice the slabs for the same tile count.  band2 word: column
-// (col_bits) | rank (4) | row (32 - col_bits - 4).
-// wide3 (cband only): 16K-row blocks, 12160-column windows and three chunks per wave
-// per band (48 chunks, 3072 terms): a third fewer bands -- each band pays a fixed
-// barrier-and-latency chain -- in the same LDS (64 KiB of sums, two 47.5 KiB x
-// windows, the table in ONE copy: its bank conflicts are spread by the builder like
-// those of the x and accumulator reads).  Its cband word: column (14) | id (8) | row
-// - base (9: a chunk's rows span < 512) | continuation (1).
+// Tile geometry (kernels_band2.hip).  wide: 16K-row blocks, 8192-column windows (the tile's
+// block sums in 64 KiB of LDS, two 32 KiB x windows), 32-chunk bands; dma3: 7680-column
+// windows in three buffers staged by a loader wave, 30-chunk bands.  band2 word: column
+// (col_bits) | rank (4) | row (32 - col_bits - 4); cband word: column (cb_col) | id (8) | row
+// - base (23 - cb_col) | continuation (1).  The builder takes any geometry of this form (the
+// ASan test builds tall, three- and six-chunk ones too); the kernel only these two -- the
+// others measured slower (tall, wide3, half2, dma3 tall, dmaw: DESIGN.md §3.4b).
 struct B2Geom {
     int32_t block_rows, window, col_bits;
     int32_t cpw = 2;          // chunks per wave per band
@@ -127,37 +122,12 @@ struct B2Geom {
     constexpr int32_t cb_row_span() const { return 1 << (31 - kCbIdBits - cb_col); }
 };
 constexpr B2Geom kB2Wide{1 << 14, 8192, 14};
-constexpr B2Geom kB2TallB2{1 << 15, 4096, 13};
-constexpr B2Geom kB2TallCb{1 << 15, 3840, 13, 2, kCbColBits, 1};
-constexpr B2Geom kB2Wide3Cb{1 << 14, 12160, 14, 3, 14, 1};
-// half2 (cband only): 8K-row blocks (32 KiB of sums) and 15872-column windows (2 x 62 KiB),
-// the table in 4 copies -- 160 KiB of LDS exactly.  Config 2 takes 2 slabs of 512K columns
-// (128 blocks x 2 = 256 tiles): twice the x per term of the wide geometry, but each tile hands
-// off half its sums to ONE sibling instead of three quarters to three.
-constexpr B2Geom kB2Half2Cb{1 << 13, 15872, 14, 2, 14, 4};
-// dma3 (cband only): wave 15 stages the x windows by LDS-DMA two bands ahead into three
-// 30 KiB buffers (7680 columns) and applies nothing; waves 0-14 apply chunks 2w, 2w+1 of
-// 30-chunk bands and never touch x in registers.  LDS: 3 x 30 KiB + 64 KiB + 4 table copies.
+// dma3: wave 15 stages the x windows by LDS-DMA two bands ahead into three 30 KiB buffers
+// (7680 columns) and applies nothing; waves 0-14 apply chunks 2w, 2w+1 of 30-chunk bands and
+// never touch x in registers.  LDS: 3 x 30 KiB + 64 KiB + 4 table copies.
 constexpr B2Geom kB2Dma3Cb{1 << 14, 7680, 13, 2, 13, 4, 30};
 // dma3 for 8-byte band2 entries (word + fp32 value): the same loader and 30-chunk bands.
 constexpr B2Geom kB2Dma3B2{1 << 14, 7680, 13, 2, kCbColBits, 1, 30};
-// dma3 with 7168-column windows: 4 KiB freed for 8 table copies (development A/B).
-constexpr B2Geom kB2Dma3tCb{1 << 14, 7168, 13, 2, 13, 8, 30};
-// dma3 tall (cband only): 32K-row blocks (128 KiB of sums), three 2560-column buffers (30 KiB),
-// the table in one copy -- 159 KiB.  Half the x bytes per term of dma3: the band loop is bound
-// by the x windows' L2 -> LDS traffic, not by the apply.  20-chunk bands
-// (waves 0-9 apply, 10-14 idle at the barriers), 12-bit columns and 11-bit row offsets (a chunk's
-// rows span < 2048).
-constexpr B2Geom kB2Dma3TallCb{1 << 15, 2560, 13, 2, 12, 1, 20};
-// dmaw (cband only; round 5): eight loader waves (8-15) stage 11520-column (45 KiB) windows by
-// LDS-DMA into TWO buffers, window q+1 issued at band q; waves 0-7 apply six chunks each of
-// 48-chunk bands, their entries four bands ahead.  One loader wave issues LDS-DMA at ~50 GB/s
-// per CU, two at ~95, four or more at ~113-117 (profiles/r05_xstream_flow.txt), and wider
-// windows cut the bands per tile from 36 to 23.  14-bit columns, 9-bit row offsets (a chunk's
-// rows span < 512).  LDS: 2 x 45 KiB + 64 KiB + 4 table copies = 158 KiB.
-constexpr B2Geom kB2DmawCb{1 << 14, 11520, 14, 6, 14, 4, 48};
-// dmaw4: the same windows, four loader waves (12-15) and twelve applying waves of four chunks.
-constexpr B2Geom kB2Dmaw4Cb{1 << 14, 11520, 14, 4, 14, 4, 48};
 
 struct Band2Host {
     bool codebook = false;               // cband encoding (ent: 2048 words per band)

@@ -15,6 +15,14 @@
 
 using namespace smamd;
 
+// Builder-only geometries (the kernel runs wide and dma3): tall tiles, three and six chunks
+// per wave -- the builder's parameterisation (row and column field widths, chunk counts).
+constexpr B2Geom kB2TallB2{1 << 15, 4096, 13};
+constexpr B2Geom kB2TallCb{1 << 15, 3840, 13, 2, kCbColBits, 1};
+constexpr B2Geom kB2Wide3Cb{1 << 14, 12160, 14, 3, 14, 1};
+constexpr B2Geom kB2DmawCb{1 << 14, 11520, 14, 6, 14, 4, 48};
+
+
 static int check_layout(const std::vector<int32_t> &rp, const std::vector<int32_t> &col,
                         const std::vector<float> &val, int64_t n_rows, int64_t n_cols, int slabs,
                         bool expect_ok, B2Geom geom = kB2Wide, int permille = 1000) {

@@ -123,20 +123,3 @@ def test_gcb_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gcb_asan: ok" in r.stdout
-
-
-@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
-def test_ro_builder_under_asan(tmp_path):
-    """Row-owner band builder (ro.cpp): every term once, each row's terms in ascending column
-    order along its wave's stream, rows inside the owning wave, windows non-decreasing."""
-    exe = tmp_path / "ro_asan"
-    src = [os.path.join(ROOT, "tests", "native", "ro_asan.cpp"),
-           os.path.join(ROOT, "sparsematrix_amd", "csrc", "ro.cpp"),
-           os.path.join(ROOT, "sparsematrix_amd", "csrc", "band2.cpp")]
-    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
-                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
-                    *src, "-o", str(exe), "-pthread"], check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
-                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "ro_asan: ok" in r.stdout

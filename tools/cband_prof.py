@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-phase cycles of the cband SpMV on config 2 (development build:
-SM_LIB_PATH=build/dev/libsparsematrix_amd.so SM_BAND2_ABLATE=1024): every launch prints
-the cycles per wave of the prologue, of each band-loop phase and of the epilogue.
+SM_LIB_PATH=build/dev/libsparsematrix_amd.so SM_BAND2_PROF=1 -- dma3's cycles per band of
+every phase, applying waves and loader -- or SM_BAND2_PROF=2 -- the per-tile timeline; add
+SM_B2_TS_DUMP=1 for every tile's line).
 Extra arguments: build options as key=value (e.g. band_slabs=2)."""
 import os
 import sys
