@@ -219,10 +219,42 @@ void balance_chunks(std::vector<std::vector<Seg>> &cs, int nc, const int32_t *co
     };
     for (int c = 0; c < nc; c++) stats(c);
     constexpr int hot = 3;
+    // Per iteration, b's singles are tabulated once (structure of arrays: index, row, banks,
+    // b's span without it, the a/b bank-count differences of its banks); for every hot single
+    // of a, one vectorisable pass scores them all (ineligible: INT32_MAX) and the first least
+    // score wins.  Same swap as the plain double loop: the first (i, j) of least d < 0.
+    // Row windows: a chunk whose other rows span [mn, mx] (empty: mn = INT32_MAX) takes a row r
+    // iff max(mx, r) - min(mn, r) < span, i.e. r in [mx - span + 1, mn + span - 1] when mx - mn
+    // < span (always: a subset of a chunk's rows), any r when empty.
+    auto win_lo = [&](int32_t mn, int32_t mx) { return mn == INT32_MAX ? INT32_MIN : mx - span + 1; };
+    auto win_hi = [&](int32_t mn, int32_t mx) { return mn == INT32_MAX ? INT32_MAX : mn + span - 1; };
+    int32_t cj[64], crl[64], clo[64], chi[64], cxt[64], cyt[64], cpx[64], cpy[64], dv[64];
     for (int a = 0; a + 1 < nc; a++) {
         const int b = a + 1;
         for (int it = 0; it < 16; it++) {
             Ch &A = ch[(size_t)a], &B = ch[(size_t)b];
+            int nt = 0;
+            for (int j = 0; j < (int)cs[(size_t)b].size(); j++) {
+                const Seg &t = cs[(size_t)b][(size_t)j];
+                if (t.n != 1) continue;
+                const int xt = xb(t), yt = t.rl & 31;
+                const int32_t bmn = t.rl == B.mn ? B.mn2 : B.mn, bmx = t.rl == B.mx ? B.mx2 : B.mx;
+                cj[nt] = j;
+                crl[nt] = t.rl;
+                clo[nt] = win_lo(bmn, bmx);
+                chi[nt] = win_hi(bmn, bmx);
+                if (bmn != INT32_MAX && bmx - bmn >= span) clo[nt] = INT32_MAX;   // (never: see above)
+                cxt[nt] = xt;
+                cyt[nt] = yt;
+                cpx[nt] = A.cx[xt] - B.cx[xt];
+                cpy[nt] = A.cy[yt] - B.cy[yt];
+                nt++;
+            }
+            int minpx = INT32_MAX, minpy = INT32_MAX;   // lower bound of any single's best d
+            for (int k = 0; k < nt; k++) {
+                minpx = std::min(minpx, cpx[k]);
+                minpy = std::min(minpy, cpy[k]);
+            }
             int best_i = -1, best_j = -1, best = 0;
             for (int i = 0; i < (int)cs[(size_t)a].size(); i++) {
                 const Seg &s_ = cs[(size_t)a][(size_t)i];
@@ -230,19 +262,24 @@ void balance_chunks(std::vector<std::vector<Seg>> &cs, int nc, const int32_t *co
                 const int xs = xb(s_), ys = s_.rl & 31;
                 if (A.cx[xs] < hot && A.cy[ys] < hot) continue;
                 const int32_t amn = s_.rl == A.mn ? A.mn2 : A.mn, amx = s_.rl == A.mx ? A.mx2 : A.mx;
-                for (int j = 0; j < (int)cs[(size_t)b].size(); j++) {
-                    const Seg &t = cs[(size_t)b][(size_t)j];
-                    if (t.n != 1) continue;
-                    const int xt = xb(t), yt = t.rl & 31;
-                    // spans after the swap
-                    const int32_t bmn = t.rl == B.mn ? B.mn2 : B.mn, bmx = t.rl == B.mx ? B.mx2 : B.mx;
-                    if (std::max(amx, t.rl) - std::min(amn, t.rl) >= span) continue;
-                    if (std::max(bmx, s_.rl) - std::min(bmn, s_.rl) >= span) continue;
-                    int d = 0;   // change of the sums of squares (x and y, both chunks)
-                    if (xs != xt) d += 2 * (A.cx[xt] - A.cx[xs] + 1) + 2 * (B.cx[xs] - B.cx[xt] + 1);
-                    if (ys != yt) d += 2 * (A.cy[yt] - A.cy[ys] + 1) + 2 * (B.cy[ys] - B.cy[yt] + 1);
-                    if (d < best) { best = d; best_i = i; best_j = j; }
+                if (amn != INT32_MAX && amx - amn >= span) continue;   // (never: see above)
+                const int32_t alo = win_lo(amn, amx), ahi = win_hi(amn, amx), srl = s_.rl;
+                // d = 2 (A.cx[xt] - A.cx[xs] + 1) + 2 (B.cx[xs] - B.cx[xt] + 1) if xs != xt, + the same in y
+                const int qx = B.cx[xs] - A.cx[xs] + 2, qy = B.cy[ys] - A.cy[ys] + 2;
+                if (nt == 0 || 2 * std::min(0, minpx + qx) + 2 * std::min(0, minpy + qy) >= best) continue;
+                for (int k = 0; k < nt; k++) {   // branch-free: vectorises
+                    const int d = 2 * (cpx[k] + qx) * (int)(xs != cxt[k]) + 2 * (cpy[k] + qy) * (int)(ys != cyt[k]);
+                    const int ok = (int)(crl[k] >= alo) & (int)(crl[k] <= ahi) & (int)(srl >= clo[k]) & (int)(srl <= chi[k]);
+                    dv[k] = ok ? d : INT32_MAX;
                 }
+                int mn = INT32_MAX;
+                for (int k = 0; k < nt; k++) mn = std::min(mn, dv[k]);
+                if (mn >= best) continue;
+                int k = 0;
+                while (dv[k] != mn) k++;
+                best = mn;
+                best_i = i;
+                best_j = cj[k];
             }
             if (best_i < 0) break;
             std::swap(cs[(size_t)a][(size_t)best_i], cs[(size_t)b][(size_t)best_j]);
