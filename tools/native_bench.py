@@ -3,7 +3,9 @@
 the CSR paths of the same matrix: config 1 (1024^2, 1 %), 16k^2 at 0.1 % (fillers
 dominate the stream), and denser cases where the 2-byte stream beats 8-byte CSR.
 Median of 50 launches with HIP events, m = 1 and m = 32; matrices built from the dense
-uint8 index exactly as the reference's CopyForm (Trans)."""
+uint8 index exactly as the reference's CopyForm (Trans).  Filters (for profiling runs):
+NATIVE_CASES (substrings of the case names, comma-separated), NATIVE_M ("1,32"),
+NATIVE_ALGOS ("native,auto,parity")."""
 import os
 import sys
 
@@ -24,16 +26,21 @@ def main():
              ("4096^2 25%", 4096, 0.25), ("8192^2 5%", 8192, 0.05)]
     print(f"{'case':22s} {'m':>3s} {'entries':>10s} {'nnz':>10s} {'native us':>10s} "
           f"{'auto us':>9s} {'parity us':>10s}")
+    sel = [c for c in os.environ.get("NATIVE_CASES", "").split(",") if c]
+    if sel:
+        cases = [c for c in cases if any(s in c[0] for s in sel)]
+    ms = [int(v) for v in os.environ.get("NATIVE_M", "1,32").split(",")]
+    algos = os.environ.get("NATIVE_ALGOS", "native,auto,parity").split(",")
     for name, n, dens in cases:
         rng = np.random.default_rng(n)
         dm = np.where(rng.random((n, n)) < dens, rng.integers(0, 255, (n, n)), 255).astype(np.uint8)
         M = sm.SparseMatrix(dm, n, n, n, table, 255, sm.SblasTrans)
         info = M.info()
-        for m in (1, 32):
+        for m in ms:
             A = torch.rand(m * n, device="cuda") * 2 - 1
             C = torch.rand(m * n, device="cuda") * 2 - 1
-            res = {}
-            for algo in ("native", "auto", "parity"):
+            res = {"native": float("nan"), "auto": float("nan"), "parity": float("nan")}
+            for algo in algos:
                 for _ in range(5):
                     M.AddMatMat(A, m, n, C, n, 1.0, 1.0, algo=algo)
                 torch.cuda.synchronize()
