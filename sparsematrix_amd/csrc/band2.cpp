@@ -108,28 +108,40 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
             for (int32_t j = 0; j < g.n; j++) put(g, j, next++);
     // Singles: greedy, most contended banks first (pairwise swaps afterwards measured
     // 2.65 / 2.44 vs 2.70 / 2.48 cycles per half-wave read, tools/band2_banks.cpp: not kept).
-    std::vector<const Seg *> single;
+    // Fixed arrays (a chunk holds <= 64 segments): no allocation per chunk.
+    const Seg *single[64];
+    int ns = 0;
     for (const Seg &g : segs)
-        if (g.n == 1) single.push_back(&g);
-    const int ns = (int)single.size();
+        if (g.n == 1) single[ns++] = &g;
     if (ns == 0) return;
     uint8_t xcnt[32] = {}, ycnt[32] = {}, tcnt[32] = {};
-    std::vector<uint8_t> sx((size_t)ns), sy((size_t)ns), st((size_t)ns), half((size_t)ns);
+    uint8_t sx[64], sy[64], st[64], half[64];
     for (int i = 0; i < ns; i++) {
-        sx[(size_t)i] = (uint8_t)((col[single[(size_t)i]->s] - clo_al) & 31);
-        sy[(size_t)i] = (uint8_t)(single[(size_t)i]->rl & 31);
-        st[(size_t)i] = tab_banks ? (uint8_t)(ids[single[(size_t)i]->s] & 31) : 0;
-        xcnt[sx[(size_t)i]]++;
-        ycnt[sy[(size_t)i]]++;
-        tcnt[st[(size_t)i]]++;
+        sx[i] = (uint8_t)((col[single[i]->s] - clo_al) & 31);
+        sy[i] = (uint8_t)(single[i]->rl & 31);
+        st[i] = tab_banks ? (uint8_t)(ids[single[i]->s] & 31) : 0;
+        xcnt[sx[i]]++;
+        ycnt[sy[i]]++;
+        tcnt[st[i]]++;
     }
-    std::vector<int> order((size_t)ns);
-    for (int i = 0; i < ns; i++) order[(size_t)i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-        const int wa = xcnt[sx[(size_t)a]] + ycnt[sy[(size_t)a]] + (tab_banks ? tcnt[st[(size_t)a]] : 0);
-        const int wb = xcnt[sx[(size_t)b]] + ycnt[sy[(size_t)b]] + (tab_banks ? tcnt[st[(size_t)b]] : 0);
-        return wa > wb;
-    });
+    // Most contended first, ties in segment order: a stable counting sort on the weight.
+    int order[64];
+    {
+        int w[64], cnt[3 * 64 + 2] = {};
+        int wmax = 0;
+        for (int i = 0; i < ns; i++) {
+            w[i] = xcnt[sx[i]] + ycnt[sy[i]] + (tab_banks ? tcnt[st[i]] : 0);
+            cnt[w[i]]++;
+            wmax = std::max(wmax, w[i]);
+        }
+        int at = 0;
+        for (int v = wmax; v >= 0; v--) {   // start offsets, heaviest first
+            const int c = cnt[v];
+            cnt[v] = at;
+            at += c;
+        }
+        for (int i = 0; i < ns; i++) order[cnt[w[i]]++] = i;
+    }
     int free_in[2] = {0, 0};
     for (int l = 0; l < 64; l++)
         if (!used[l]) free_in[l >> 5]++;
@@ -139,8 +151,9 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
         int free_hc[2][4] = {};
         for (int l = 0; l < 64; l++)
             if (!used[l]) free_hc[l >> 5][l & 3]++;
-        std::vector<uint8_t> cls((size_t)ns);
-        for (int i : order) {
+        uint8_t cls[64];
+        for (int oi = 0; oi < ns; oi++) {
+            const int i = order[oi];
             const uint32_t id = ids[single[(size_t)i]->s];
             int best = -1, bcls = 0, bcost = 1 << 30;
             for (int h = 0; h < 2; h++)
@@ -165,7 +178,8 @@ void emit_chunk(uint32_t *band_ent, int c, const std::vector<Seg> &segs, const i
         }
         return;
     }
-    for (int i : order) {
+    for (int oi = 0; oi < ns; oi++) {
+        const int i = order[oi];
         int best = -1, bcost = 1 << 30;
         for (int h = 0; h < 2; h++) {
             if (free_in[h] == 0) continue;
