@@ -21,6 +21,7 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--ab-env", default="SM_SPMM_OLD",
                     help="variable toggled 1 (\"old\") / 0 (\"new\"), e.g. SM_SPMM_NT")
+    ap.add_argument("--algo", default="auto", help="sm_spmm algorithm of the env A/B (e.g. mfma)")
     ap.add_argument("--algos", default="",
                     help="compare sm_spmm algorithms instead, e.g. auto,mfma (old = the first)")
     args = ap.parse_args()
@@ -45,7 +46,7 @@ def main() -> None:
         res = {}
         algos = args.algos.split(",") if args.algos else None
         for old in ("1", "0"):
-            algo = "auto"
+            algo = args.algo
             if algos:
                 algo = algos[0] if old == "1" else algos[1]
             else:
