@@ -90,12 +90,17 @@ typedef enum sm_algo {
                              exceeds SM_SERIAL_ROW_MAX terms, else PARITY.  SpMM and
                              AddMatMat with m > 1: the row-panel kernels (every row in
                              order).  What the reference's C++ surface (libsblas) runs. */
-    SM_ALGO_MFMA = 8      /* SpMM with n_rhs == 32 only: 16-row tiles on the matrix cores
+    SM_ALGO_MFMA = 8,     /* SpMM with n_rhs == 32 only: 16-row tiles on the matrix cores
                              (v_mfma_f32_16x16x4_f32, four terms per step), one fused
                              multiply-add per term: within the sum|terms| bound, not
                              bit-identical; X must be finite (a non-finite X row makes
                              the tile's other outputs NaN).  SM_ERR_NOT_SUPPORTED for
                              other shapes and for SpMV.                                */
+    SM_ALGO_MERGE = 9     /* SpMV by merge path (Merrill & Garland): every workgroup and
+                             thread an equal share of rows + terms, rows cut anywhere.
+                             A row inside one thread's share is summed in stored order
+                             (bit-identical); cut rows join their parts in a fixed order
+                             (within the sum|terms| bound, deterministic).  SpMM: as AUTO. */
 } sm_algo;
 
 /* Rows with at most this many terms are summed in reference order by the

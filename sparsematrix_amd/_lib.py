@@ -32,7 +32,7 @@ SM_ERR_NO_DEVICE = 7
 # sm_trans / sm_algo
 SM_NO_TRANS, SM_TRANS = 0, 1
 ALGOS = {"auto": 0, "parity": 1, "stream": 2, "vector": 3, "xband": 4, "sell": 5, "native": 6,
-         "exact": 7, "mfma": 8}
+         "exact": 7, "mfma": 8, "merge": 9}
 
 # Every symbol include/sparsematrix.h declares (tests check the .so exports them).
 EXPORTS = (

@@ -100,6 +100,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->d_col);
     (void)hipFree(m->d_val);
     (void)hipFree(m->plan.d_tiles);
+    (void)hipFree(m->plan.d_merge);
     (void)hipFree(m->plan.d_long_rows);
     (void)hipFree(m->plan.d_long_ptr);
     (void)hipFree(m->plan.d_chunks);
@@ -972,6 +973,8 @@ sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     p.max_row_nnz = ph.max_row_nnz;
     p.avg_row_nnz = ph.avg_row_nnz;
     SM_TRY_HIP(dev_alloc(&p.d_tiles, p.n_tiles, m->device_bytes));
+    if (m->n_rows > 0 && m->nnz > 0)   // merge-path records (SM_ALGO_MERGE), 32 B per workgroup
+        SM_TRY_HIP(dev_alloc(&p.d_merge, merge_blocks(m->n_rows, m->nnz), m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_chunks, p.n_chunks, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_partials, p.n_chunks, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_long_rows, p.n_long, m->device_bytes));
@@ -1648,15 +1651,16 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
     }
     if (algo == SM_ALGO_MFMA) return fail(SM_ERR_NOT_SUPPORTED, "SM_ALGO_MFMA is an SpMM algorithm (n_rhs = 32)");
     const int ai = algo == SM_ALGO_EXACT ? exact_algo(m, ((uintptr_t)x % 16) == 0) : (int)algo;
-    if ((ai < SM_ALGO_AUTO || ai > SM_ALGO_SELL) && ai != kAlgoExactSell)
+    if ((ai < SM_ALGO_AUTO || ai > SM_ALGO_SELL) && ai != kAlgoExactSell && ai != SM_ALGO_MERGE)
         return fail(SM_ERR_INVALID_ARG, "unknown algo %d", (int)algo);
     // The matrix's SpMV scratch (sm_internal.h): SpMVs that use it run one after the
     // other on the device, whatever stream or thread issues them.
     const Plan &pl = m->plan;
-    const bool scratch = ai != SM_ALGO_PARITY && ai != SM_ALGO_VECTOR &&
-                         ((pl.xb.n_blocks > 0 && pl.xb.n_slabs > 1) || pl.n_relabel > 0 ||
-                          (pl.hot.n_blocks > 0 && pl.hot.n_slabs > 1) ||
-                          pl.sell.n_long > 0 || pl.n_long > 0);
+    const bool scratch = ai == SM_ALGO_MERGE ||
+                         (ai != SM_ALGO_PARITY && ai != SM_ALGO_VECTOR &&
+                          ((pl.xb.n_blocks > 0 && pl.xb.n_slabs > 1) || pl.n_relabel > 0 ||
+                           (pl.hot.n_blocks > 0 && pl.hot.n_slabs > 1) ||
+                           pl.sell.n_long > 0 || pl.n_long > 0));
     std::unique_lock<std::mutex> lk(m->scratch_mu, std::defer_lock);
     bool ordered = false;
     if (scratch) {
@@ -1726,6 +1730,10 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
                                m->plan.d_partials, s);
         break;
+    case SM_ALGO_MERGE:   // merge path over the CSR arrays (kernels_merge.hip)
+        e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
+                              m->plan.d_merge, s);
+        break;
     case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
         const float *xs = x;
         if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns
@@ -1774,7 +1782,7 @@ sm_status sm_spmm(const sm_matrix *m, int32_t n_rhs, float alpha, const float *X
     }
     const bool vec_ok = n_rhs % 4 == 0 && n_rhs <= 128 && ldx % 4 == 0 && ldy % 4 == 0 &&
                         ((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0;
-    if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND || algo == SM_ALGO_EXACT)
+    if (algo == SM_ALGO_SELL || algo == SM_ALGO_XBAND || algo == SM_ALGO_EXACT || algo == SM_ALGO_MERGE)
         algo = SM_ALGO_AUTO;   // SpMV layouts; the SpMM kernels keep every row's order
     if ((algo == SM_ALGO_AUTO || algo == SM_ALGO_STREAM || algo == SM_ALGO_VECTOR) && vec_ok)
         e = launch_spmm_rowpanel(n, n_rhs, m->d_row_ptr, m->d_col, m->d_val, (int32_t)m->nnz, X,

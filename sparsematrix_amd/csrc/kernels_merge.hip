@@ -1,0 +1,225 @@
+// kernels_merge.hip -- merge-path CSR SpMV (SM_ALGO_MERGE; north_star's "merge-path row
+// balancing").
+//
+// The work of y = alpha * B x + beta * y is the merge of two lists: the n row ends (rp[1..n])
+// and the nnz term indices 0..nnz-1.  Every workgroup takes an equal slice of kMgTile merge
+// items and every thread kMgIpt of them, wherever rows start and end -- a row of 10^5 terms
+// and 10^5 empty rows cost the same (Merrill & Garland's merge-based SpMV):
+//   1. the workgroup finds its slice's (row, term) corner by a binary search on its diagonal;
+//   2. it stages the slice's terms fl(x[col] * fl(v * alpha)) (coalesced col / val loads, the
+//      x gathers back to back) and row ends in LDS;
+//   3. each thread finds its own corner in LDS and walks its items: a term adds to the running
+//      sum, a row end finishes the row.  A row whose first term the thread saw started from
+//      beta*y and is written at once, in the reference's order (kernel.cc:780-796) -- bit-exact;
+//   4. rows cut between threads: each thread leaves the open row's partial (a "tail") and the
+//      partial of a row it finished but did not start (a "head"); a segmented scan over the
+//      tails (fixed tree order) joins the cut rows inside the workgroup, y = (start part +
+//      middle parts) + end part -- within 1e-6 * sum|terms| of the reference, deterministic;
+//   5. rows cut between workgroups leave one record per workgroup (its first row's end part,
+//      its last row's open part); spmv_merge_fixup_kernel adds them in workgroup order.
+#include "sm_internal.h"
+#include "xband_dev.h"
+
+namespace smamd {
+namespace {
+
+constexpr int kMgThreads = 256;
+constexpr int kMgIpt = 8;                          // merge items per thread
+constexpr int kMgTile = kMgThreads * kMgIpt;       // 2048 per workgroup
+
+// Corner of merge diagonal d: the number of row ends (row) and terms (nz) before it.
+// rend[i] = end of row i; a row end is taken before a term with the same index.
+template <typename RendT>
+__device__ __forceinline__ void merge_corner(int64_t d, RendT rend, int64_t n, int64_t nnz, int64_t &row,
+                                             int64_t &nz) {
+    int64_t lo = d - nnz > 0 ? d - nnz : 0, hi = d < n ? d : n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)rend(mid) <= d - mid - 1) lo = mid + 1;
+        else hi = mid;
+    }
+    row = lo;
+    nz = d - lo;
+}
+
+__global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
+    int32_t n, int32_t nnz, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ x, float *__restrict__ y, float alpha, float beta,
+    MergeRec *__restrict__ rec) {
+    __shared__ float s_term[kMgTile];
+    __shared__ int32_t s_rend[kMgTile];
+    __shared__ int32_t s_corner[4];
+    __shared__ int32_t t_row[kMgThreads], t_flag[2][kMgThreads], t_sf[2][kMgThreads];
+    __shared__ float t_val[2][kMgThreads];
+    const int tid = threadIdx.x;
+    const int64_t total = (int64_t)n + nnz;
+    const int64_t d0 = (int64_t)blockIdx.x * kMgTile;
+    if (tid < 2) {
+        const int64_t d = tid == 0 ? d0 : (d0 + kMgTile < total ? d0 + kMgTile : total);
+        int64_t r, z;
+        merge_corner(d, [&](int64_t i) { return rp[i + 1]; }, n, nnz, r, z);
+        s_corner[2 * tid] = (int32_t)r;
+        s_corner[2 * tid + 1] = (int32_t)z;
+    }
+    __syncthreads();
+    const int32_t r0 = s_corner[0], z0 = s_corner[1], r1 = s_corner[2], z1 = s_corner[3];
+    const int32_t tile_rows = r1 - r0, tile_nnz = z1 - z0;
+    // Stage: the slice's terms (every load issued before the first is used) and row ends.
+    {
+        int32_t c[kMgIpt];
+        float v[kMgIpt];
+#pragma unroll
+        for (int k = 0; k < kMgIpt; ++k) {
+            const int32_t z = k * kMgThreads + tid;
+            const int32_t gz = z < tile_nnz ? z0 + z : 0;   // nnz > 0 here
+            c[k] = col[gz];
+            v[k] = val[gz];
+        }
+#pragma unroll
+        for (int k = 0; k < kMgIpt; ++k) {
+            const int32_t z = k * kMgThreads + tid;
+            const float xv = x[c[k]];
+            if (z < tile_nnz) s_term[z] = __fmul_rn(xv, __fmul_rn(v[k], alpha));
+        }
+#pragma unroll
+        for (int k = 0; k < kMgIpt; ++k) {
+            const int32_t r = k * kMgThreads + tid;
+            if (r < tile_rows) s_rend[r] = rp[r0 + 1 + r] - z0;
+        }
+    }
+    const int32_t rstart0 = rp[r0] - z0;   // the slice's first row's start (<= 0)
+    __syncthreads();
+
+    // This thread's items [dt, de) of the slice and its corner (ri, zi) in it.
+    const int32_t items = tile_rows + tile_nnz;
+    const int32_t dt = min(tid * kMgIpt, items), de = min(dt + kMgIpt, items);
+    int64_t ri64, zi64;
+    merge_corner(dt, [&](int64_t i) { return s_rend[i]; }, tile_rows, tile_nnz, ri64, zi64);
+    int32_t ri = (int32_t)ri64, zi = (int32_t)zi64;
+    auto y_init = [&](int32_t row) -> float {   // beta * y (multiplied iff beta != 1, kernel.cc:10-29)
+        if (row >= n) return 0.0f;
+        const float yv = y[row];
+        return beta != 1.0f ? __fmul_rn(yv, beta) : yv;
+    };
+    const int32_t first_row = r0 + ri;
+    bool fresh = dt < de && (ri == 0 ? rstart0 : s_rend[ri - 1]) == zi;   // the thread sees the row's start
+    float acc = fresh ? y_init(first_row) : -0.0f;
+    bool open = false, has_head = false;
+    float head = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kMgIpt; ++k) {
+        if (dt + k < de) {
+            if (ri < tile_rows && s_rend[ri] <= zi) {   // row r0 + ri ends
+                if (fresh) {
+                    y[r0 + ri] = acc;
+                } else {   // the thread's first row, started before it
+                    has_head = true;
+                    head = acc;
+                }
+                ++ri;
+                fresh = true;
+                open = false;
+                acc = y_init(r0 + ri);
+            } else {
+                acc = __fadd_rn(acc, s_term[zi]);
+                ++zi;
+                open = true;
+            }
+        }
+    }
+    // Tails: a segmented inclusive scan over threads (segments = runs of one cut row; a run
+    // starts at a thread that saw the row's start or follows a thread without that row).
+    t_row[tid] = open ? r0 + ri : -1;
+    __syncthreads();
+    {
+        const bool start = !open || tid == 0 || t_row[tid - 1] != t_row[tid] || fresh;
+        t_val[0][tid] = open ? acc : 0.0f;
+        t_flag[0][tid] = start;
+        t_sf[0][tid] = open && fresh;
+    }
+    __syncthreads();
+    int cur = 0;
+#pragma unroll
+    for (int d = 1; d < kMgThreads; d <<= 1) {
+        float v = t_val[cur][tid];
+        int f = t_flag[cur][tid], sf = t_sf[cur][tid];
+        if (tid >= d && !f) {
+            v = __fadd_rn(t_val[cur][tid - d], v);
+            sf = t_sf[cur][tid - d];
+            f = t_flag[cur][tid - d];
+        }
+        t_val[cur ^ 1][tid] = v;
+        t_flag[cur ^ 1][tid] = f;
+        t_sf[cur ^ 1][tid] = sf;
+        cur ^= 1;
+        __syncthreads();
+    }
+    // Heads: the thread finished a row started before it -- join it with the tails before.
+    // Only the workgroup's first row can have started in an earlier workgroup; its end part
+    // goes to the workgroup's record.
+    if (tid == 0) s_corner[0] = -1;
+    __syncthreads();
+    if (has_head) {
+        float tot = head;
+        bool started_here = false;
+        if (tid > 0 && t_row[tid - 1] == first_row) {
+            tot = __fadd_rn(t_val[cur][tid - 1], head);
+            started_here = t_sf[cur][tid - 1] != 0;
+        }
+        if (started_here) {
+            y[first_row] = tot;
+        } else {
+            s_corner[0] = first_row;
+            t_val[cur ^ 1][0] = tot;
+        }
+    }
+    // The workgroup's last open row (the thread holding the slice's last item).
+    const int32_t t_last = items > 0 ? (items - 1) / kMgIpt : 0;
+    if (tid == t_last) {
+        rec[blockIdx.x].last_row = open ? r0 + ri : -1;
+        rec[blockIdx.x].last_val = t_val[cur][tid];
+        rec[blockIdx.x].last_fresh = t_sf[cur][tid];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        rec[blockIdx.x].first_row = s_corner[0];
+        rec[blockIdx.x].first_val = s_corner[0] >= 0 ? t_val[cur ^ 1][0] : 0.0f;
+    }
+}
+
+// Rows cut between workgroups: workgroup m finished row R (first_row) that began in an earlier
+// one; the workgroups in between lie inside R.  y[R] = start part + middle parts + end part,
+// in workgroup order.
+__global__ void spmv_merge_fixup_kernel(int32_t n_blocks, const MergeRec *__restrict__ rec,
+                                        float *__restrict__ y) {
+    const int32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n_blocks) return;
+    const int32_t R = rec[m].first_row;
+    if (R < 0) return;
+    int32_t j = m - 1;
+    while (j > 0 && !(rec[j].last_row == R && rec[j].last_fresh)) --j;   // the start part
+    float tot = rec[j].last_val;
+    for (int32_t i = j + 1; i < m; ++i) tot = __fadd_rn(tot, rec[i].last_val);
+    y[R] = __fadd_rn(tot, rec[m].first_val);
+}
+
+}  // namespace
+
+int64_t merge_blocks(int64_t n_rows, int64_t nnz) { return (n_rows + nnz + kMgTile - 1) / kMgTile; }
+
+hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
+                             const float *x, float *y, float alpha, float beta, MergeRec *rec, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (nnz == 0) return launch_beta(y, 1, n, n, beta, s);
+    const int64_t nb = merge_blocks(n, nnz);
+    if (nb > INT32_MAX || !rec) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(spmv_merge_kernel, dim3((unsigned)nb), dim3(kMgThreads), 0, s, n, nnz, rp, col, val, x, y,
+                       alpha, beta, rec);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(spmv_merge_fixup_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, (int32_t)nb,
+                       rec, y);
+    return hipGetLastError();
+}
+
+}  // namespace smamd

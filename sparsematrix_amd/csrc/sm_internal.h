@@ -168,6 +168,21 @@ struct SweepDev {   // column-swept row blocks (sweep.h)
     int32_t table_size = 0;
 };
 
+// Merge-path SpMV, per workgroup: its first row's end part when that row began in an earlier
+// workgroup (first_row >= 0), and its last row's open part (last_row >= 0; last_fresh: the
+// part starts with the row's beta * y).
+struct MergeRec {
+    int32_t first_row;
+    float first_val;
+    int32_t last_row;
+    float last_val;
+    int32_t last_fresh;
+    int32_t pad[3];
+};
+int64_t merge_blocks(int64_t n_rows, int64_t nnz);
+hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
+                             const float *x, float *y, float alpha, float beta, MergeRec *rec, hipStream_t s);
+
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
     SellDev sell;                     // n_slices == 0 when not built
@@ -199,6 +214,8 @@ struct Plan {
     int32_t *d_perm = nullptr;        // original column -> new column (x is scattered)
     int32_t *d_rcol = nullptr;        // relabeled col_idx (nnz + kPadElems, zero tail)
     float *d_xperm = nullptr;         // x in the new numbering (one SpMV in flight)
+    // Merge-path SpMV (kernels_merge.hip): one record per workgroup (one SpMV in flight).
+    MergeRec *d_merge = nullptr;
 };
 
 // Host launchers (kernels.hip).  All return hipError_t of the launch.

@@ -1,0 +1,106 @@
+"""SM_ALGO_MERGE: merge-path SpMV (sparsematrix_amd/csrc/kernels_merge.hip; north_star's
+"merge-path row balancing").  Every workgroup takes 2048 merge items (row ends + terms) and
+every thread 8, so rows are cut anywhere.  A row whose items all fall in one thread's 8 is
+summed in stored order from beta*y -- bit-identical to the reference
+(/root/reference/src/sparse/kernel.cc:780-796, :791 for the term); cut rows join their parts
+in a fixed order: within 1e-6 * sum|terms| of the reference, and deterministic."""
+import numpy as np
+import pytest
+
+import oracle
+from gpu_util import assert_terms_close, bits, to_dev, to_host, torch_dev, uniform_csr
+
+pytestmark = pytest.mark.gpu
+
+IPT, TILE = 8, 2048   # merge items per thread / per workgroup (kernels_merge.hip)
+
+
+@pytest.fixture(scope="module")
+def sm():
+    torch_dev()
+    oracle.build()
+    import sparsematrix_amd
+    sparsematrix_amd.load()
+    return sparsematrix_amd
+
+
+def _one_thread_rows(rp):
+    """Rows whose merge items (first term .. row end) lie in one thread's group of 8."""
+    r = np.arange(rp.size - 1, dtype=np.int64)
+    start = rp[:-1].astype(np.int64) + r        # the row's first item (its first term, or its end)
+    end = rp[1:].astype(np.int64) + r           # the row-end item
+    return (start // IPT) == (end // IPT)
+
+
+def _check(sm, rp, ci, va, n_cols, alpha, beta, seed, y_special=False):
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = rng.uniform(-1, 1, rp.size - 1).astype(np.float32)
+    if y_special:
+        y0[::101] = np.nan
+        y0[1::103] = -0.0
+    outs = []
+    for _ in range(2):
+        y = to_dev(y0)
+        M.spmv(to_dev(x), y, alpha, beta, algo="merge")
+        outs.append(to_host(y))
+    got = outs[0]
+    assert np.array_equal(bits(outs[0]), bits(outs[1])), "not deterministic"
+    want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
+    one = _one_thread_rows(rp)
+    assert np.array_equal(bits(got[one]), bits(want[one])), "rows inside one thread must be bit-exact"
+    _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
+    fin = np.isfinite(want)
+    assert_terms_close(got[fin], want[fin], absum[fin])
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    return one.mean()
+
+
+@pytest.mark.parametrize("n_rows,n_cols,per_row", [(30001, 40000, 16), (5000, 1000, 3), (1, 50000, 300),
+                                                   (100003, 200000, 1)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.5), (1.3, 1.0), (0.7, 0.0)])
+def test_merge_uniform_vs_oracle(sm, n_rows, n_cols, per_row, alpha, beta):
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + per_row)
+    _check(sm, rp, ci, va, n_cols, alpha, beta, seed=7)
+
+
+def test_merge_skewed_rows_and_empty_rows(sm):
+    """Power-law rows (a few of 10^5 terms, spanning dozens of workgroups), runs of empty rows
+    (many row ends inside one thread's share), NaN and -0.0 in y."""
+    rng = np.random.default_rng(11)
+    n_rows, n_cols = 60000, 300000
+    lens = np.minimum(rng.zipf(1.6, n_rows), 4000).astype(np.int64)
+    lens[rng.random(n_rows) < 0.3] = 0
+    lens[[5, 777, 40000]] = [120000, 50000, 200000]
+    rp = np.zeros(n_rows + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, int(k), replace=False)) if k else np.zeros(0, np.int64)
+                         for k in lens]).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    for alpha, beta in ((1.0, 0.5), (2.0, 0.0)):
+        share = _check(sm, rp.astype(np.int32), ci, va, n_cols, alpha, beta, seed=13, y_special=True)
+    assert share > 0.3   # a real share of rows takes the bit-exact path
+
+
+def test_merge_config2_full_size(sm):
+    """BASELINE config 2 at full size through SM_ALGO_MERGE: within the bound everywhere,
+    bit-exact on the rows inside one thread (sampled check on the whole vector)."""
+    torch = torch_dev()
+    import sparsematrix_amd.synth as synth
+    n = 1 << 20
+    rp, ci, va = synth.uniform_rows_device(n, n, 16, seed=2)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = y0.clone()
+    M.spmv(x, y, 1.0, 0.5, algo="merge")
+    got = to_host(y)
+    rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+    xh, y0h = to_host(x), to_host(y0)
+    want = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.0, 0.5, threads=16)
+    one = _one_thread_rows(rph)
+    assert np.array_equal(bits(got[one]), bits(want[one]))
+    _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.0, 0.5)
+    assert_terms_close(got, want, absum)
