@@ -101,6 +101,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->d_val);
     (void)hipFree(m->plan.d_tiles);
     (void)hipFree(m->plan.d_merge);
+    (void)hipFree(m->plan.d_merge_corner);
     (void)hipFree(m->plan.d_long_rows);
     (void)hipFree(m->plan.d_long_ptr);
     (void)hipFree(m->plan.d_chunks);
@@ -973,8 +974,14 @@ sm_status upload_plan(sm_matrix *m, const int32_t *rp_host) {
     p.max_row_nnz = ph.max_row_nnz;
     p.avg_row_nnz = ph.avg_row_nnz;
     SM_TRY_HIP(dev_alloc(&p.d_tiles, p.n_tiles, m->device_bytes));
-    if (m->n_rows > 0 && m->nnz > 0)   // merge-path records (SM_ALGO_MERGE), 32 B per workgroup
-        SM_TRY_HIP(dev_alloc(&p.d_merge, merge_blocks(m->n_rows, m->nnz), m->device_bytes));
+    if (m->n_rows > 0 && m->nnz > 0) {   // merge path (SM_ALGO_MERGE): slice corners, 32 B records
+        const int64_t nb = merge_blocks(m->n_rows, m->nnz);
+        std::vector<int32_t> corners;
+        merge_corners(rp_host, m->n_rows, m->nnz, corners);
+        SM_TRY_HIP(dev_alloc(&p.d_merge, nb, m->device_bytes));
+        SM_TRY_HIP(dev_alloc(&p.d_merge_corner, nb + 1, m->device_bytes));
+        SM_TRY_HIP(hipMemcpy(p.d_merge_corner, corners.data(), corners.size() * 4, hipMemcpyHostToDevice));
+    }
     SM_TRY_HIP(dev_alloc(&p.d_chunks, p.n_chunks, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_partials, p.n_chunks, m->device_bytes));
     SM_TRY_HIP(dev_alloc(&p.d_long_rows, p.n_long, m->device_bytes));
@@ -1732,7 +1739,7 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         break;
     case SM_ALGO_MERGE:   // merge path over the CSR arrays (kernels_merge.hip)
         e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
-                              m->plan.d_merge, s);
+                              m->plan.d_merge_corner, m->plan.d_merge, s);
         break;
     case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
         const float *xs = x;

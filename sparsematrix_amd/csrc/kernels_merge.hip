@@ -5,7 +5,9 @@
 // and the nnz term indices 0..nnz-1.  Every workgroup takes an equal slice of kMgTile merge
 // items and every thread kMgIpt of them, wherever rows start and end -- a row of 10^5 terms
 // and 10^5 empty rows cost the same (Merrill & Garland's merge-based SpMV):
-//   1. the workgroup finds its slice's (row, term) corner by a binary search on its diagonal;
+//   1. the slices' (row, term) corners depend only on the row pointers: the plan holds them
+//      (merge_corners, binary searches on the host at creation), so a workgroup starts with
+//      two loads instead of a chain of dependent ones;
 //   2. it stages the slice's terms fl(x[col] * fl(v * alpha)) (coalesced col / val loads, the
 //      x gathers back to back) and row ends in LDS;
 //   3. each thread finds its own corner in LDS and walks its items: a term adds to the running
@@ -19,6 +21,9 @@
 //      its last row's open part); spmv_merge_fixup_kernel adds them in workgroup order.
 #include "sm_internal.h"
 #include "xband_dev.h"
+
+#include <algorithm>
+#include <vector>
 
 namespace smamd {
 namespace {
@@ -45,24 +50,15 @@ __device__ __forceinline__ void merge_corner(int64_t d, RendT rend, int64_t n, i
 __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     int32_t n, int32_t nnz, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ x, float *__restrict__ y, float alpha, float beta,
-    MergeRec *__restrict__ rec) {
+    const int2 *__restrict__ corner, MergeRec *__restrict__ rec) {
     __shared__ float s_term[kMgTile];
     __shared__ int32_t s_rend[kMgTile];
     __shared__ int32_t s_corner[4];
     __shared__ int32_t t_row[kMgThreads], t_flag[2][kMgThreads], t_sf[2][kMgThreads];
     __shared__ float t_val[2][kMgThreads];
     const int tid = threadIdx.x;
-    const int64_t total = (int64_t)n + nnz;
-    const int64_t d0 = (int64_t)blockIdx.x * kMgTile;
-    if (tid < 2) {
-        const int64_t d = tid == 0 ? d0 : (d0 + kMgTile < total ? d0 + kMgTile : total);
-        int64_t r, z;
-        merge_corner(d, [&](int64_t i) { return rp[i + 1]; }, n, nnz, r, z);
-        s_corner[2 * tid] = (int32_t)r;
-        s_corner[2 * tid + 1] = (int32_t)z;
-    }
-    __syncthreads();
-    const int32_t r0 = s_corner[0], z0 = s_corner[1], r1 = s_corner[2], z1 = s_corner[3];
+    const int2 c0 = corner[blockIdx.x], c1 = corner[blockIdx.x + 1];
+    const int32_t r0 = c0.x, z0 = c0.y, r1 = c1.x, z1 = c1.y;
     const int32_t tile_rows = r1 - r0, tile_nnz = z1 - z0;
     // Stage: the slice's terms (every load issued before the first is used) and row ends.
     {
@@ -207,14 +203,31 @@ __global__ void spmv_merge_fixup_kernel(int32_t n_blocks, const MergeRec *__rest
 
 int64_t merge_blocks(int64_t n_rows, int64_t nnz) { return (n_rows + nnz + kMgTile - 1) / kMgTile; }
 
+void merge_corners(const int32_t *rp, int64_t n_rows, int64_t nnz, std::vector<int32_t> &out) {
+    const int64_t nb = merge_blocks(n_rows, nnz), total = n_rows + nnz;
+    out.resize((size_t)(2 * (nb + 1)));
+    for (int64_t b = 0; b <= nb; ++b) {
+        const int64_t d = std::min<int64_t>(b * kMgTile, total);
+        int64_t lo = std::max<int64_t>(d - nnz, 0), hi = std::min<int64_t>(d, n_rows);
+        while (lo < hi) {   // merge_corner, on the host
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)rp[mid + 1] <= d - mid - 1) lo = mid + 1;
+            else hi = mid;
+        }
+        out[(size_t)(2 * b)] = (int32_t)lo;
+        out[(size_t)(2 * b + 1)] = (int32_t)(d - lo);
+    }
+}
+
 hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
-                             const float *x, float *y, float alpha, float beta, MergeRec *rec, hipStream_t s) {
+                             const float *x, float *y, float alpha, float beta, const int2 *corner, MergeRec *rec,
+                             hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (nnz == 0) return launch_beta(y, 1, n, n, beta, s);
     const int64_t nb = merge_blocks(n, nnz);
-    if (nb > INT32_MAX || !rec) return hipErrorInvalidValue;
+    if (nb > INT32_MAX || !rec || !corner) return hipErrorInvalidValue;
     hipLaunchKernelGGL(spmv_merge_kernel, dim3((unsigned)nb), dim3(kMgThreads), 0, s, n, nnz, rp, col, val, x, y,
-                       alpha, beta, rec);
+                       alpha, beta, corner, rec);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(spmv_merge_fixup_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, (int32_t)nb,

@@ -180,8 +180,11 @@ struct MergeRec {
     int32_t pad[3];
 };
 int64_t merge_blocks(int64_t n_rows, int64_t nnz);
+// The (row, term) corner of every workgroup's slice, blocks + 1 of them (x = row, y = term).
+void merge_corners(const int32_t *rp, int64_t n_rows, int64_t nnz, std::vector<int32_t> &out);
 hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
-                             const float *x, float *y, float alpha, float beta, MergeRec *rec, hipStream_t s);
+                             const float *x, float *y, float alpha, float beta, const int2 *corner, MergeRec *rec,
+                             hipStream_t s);
 
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
@@ -216,6 +219,7 @@ struct Plan {
     float *d_xperm = nullptr;         // x in the new numbering (one SpMV in flight)
     // Merge-path SpMV (kernels_merge.hip): one record per workgroup (one SpMV in flight).
     MergeRec *d_merge = nullptr;
+    int2 *d_merge_corner = nullptr;   // merge_blocks + 1 slice corners
 };
 
 // Host launchers (kernels.hip).  All return hipError_t of the launch.
