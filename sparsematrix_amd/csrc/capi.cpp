@@ -1738,6 +1738,13 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
                                m->plan.d_partials, s);
         break;
     case SM_ALGO_MERGE:   // merge path over the CSR arrays (kernels_merge.hip)
+        if (m->plan.n_relabel > 0) {   // skewed columns: the relabeled copy, hot x in L2 (as stream)
+            e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
+            if (e == hipSuccess)
+                e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->plan.d_rcol, m->d_val, m->plan.d_xperm, y,
+                                      alpha, beta, m->plan.d_merge_corner, m->plan.d_merge, s);
+            break;
+        }
         e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
                               m->plan.d_merge_corner, m->plan.d_merge, s);
         break;
