@@ -29,7 +29,10 @@ namespace smamd {
 namespace {
 
 constexpr int kMgThreads = 256;
-constexpr int kMgIpt = 8;                          // merge items per thread
+#ifndef SM_MERGE_IPT
+#define SM_MERGE_IPT 8
+#endif
+constexpr int kMgIpt = SM_MERGE_IPT;               // merge items per thread (A/B builds: DEV_FLAGS)
 constexpr int kMgTile = kMgThreads * kMgIpt;       // 2048 per workgroup
 
 // Corner of merge diagonal d: the number of row ends (row) and terms (nz) before it.
