@@ -104,3 +104,25 @@ def test_merge_config2_full_size(sm):
     assert np.array_equal(bits(got[one]), bits(want[one]))
     _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.0, 0.5)
     assert_terms_close(got, want, absum)
+
+
+def test_merge_edge_shapes(sm):
+    """One term in one row, a single non-empty row among many empty ones, and no terms at all
+    (beta * y only, multiplied iff beta != 1: NaN stays NaN)."""
+    rp = np.array([0, 1], np.int32)
+    _check(sm, rp, np.array([3], np.int32), np.array([0.5], np.float32), 10, 1.0, 0.5, seed=1)
+    n_rows = 5000
+    rp = np.zeros(n_rows + 1, np.int32)
+    rp[2501:] = 40
+    ci = np.arange(40, dtype=np.int32) * 3
+    va = np.linspace(-1, 1, 40).astype(np.float32)
+    _check(sm, rp, ci, va, 200, 1.3, 0.7, seed=2, y_special=True)
+    rp0 = np.zeros(n_rows + 1, np.int32)
+    M = sm.SparseMatrix.from_csr(rp0, np.zeros(0, np.int32), np.zeros(0, np.float32), 100)
+    y0 = np.random.default_rng(3).uniform(-1, 1, n_rows).astype(np.float32)
+    y0[::7] = np.nan
+    y = to_dev(y0)
+    M.spmv(to_dev(np.ones(100, np.float32)), y, 1.0, 0.25, algo="merge")
+    want = oracle.csr_spmv(rp0, np.zeros(0, np.int32), np.zeros(0, np.float32), np.ones(100, np.float32),
+                           y0, 1.0, 0.25)
+    assert np.array_equal(bits(to_host(y)), bits(want))
