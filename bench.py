@@ -516,8 +516,8 @@ def main():
                     "mfma_util": mfm.get("mfma_util") if mfm else None,
                     "mfma_insts": mfm.get("mfma_insts") if mfm else None,
                     "mfma_source": ("profiles/mfma_" + swl + "_mfma.json (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / "
-                                    "GRBM_GUI_ACTIVE of the register-operand form; the LDS form issues the "
-                                    "same MFMA stream)" if mfm else None),
+                                    "GRBM_GUI_ACTIVE, SQ_INSTS_VALU_MFMA_F32 of spmm_mfma_lds_kernel<8>)"
+                                    if mfm else None),
                     "kernel": "spmm_mfma_lds_kernel<8> (gathered X rows staged through LDS by LDS-DMA, "
                               "v_mfma_f32_16x16x4_f32 on 16-row tiles; within the sum|terms| bound, not "
                               "bit-exact; DESIGN.md §3.5)"}
