@@ -607,7 +607,8 @@ def main():
                        "nnz_per_rank": nnz,
                        "per_row": per, "replicas": replicas, "algo": args.algo,
                        "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
-                       "build_s": round(build_s, 1),
+                       "build_s": round(build_s, 1),   # every replica: generation + layout build
+                       "build_s_per_matrix": round(build_s / max(replicas, 1), 2),
                        "parallelism": f"row-partition x{world}" + (
                            f", {path}" + (": all-gather of step k+1 beside SpMV k"
                                           if overlap else "") if world > 1 else ""),
