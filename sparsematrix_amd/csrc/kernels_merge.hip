@@ -56,7 +56,8 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     const int2 *__restrict__ corner, MergeRec *__restrict__ rec) {
     __shared__ float s_term[kMgTile];
     __shared__ int32_t s_rend[kMgTile];
-    __shared__ int32_t s_corner[4];
+    __shared__ int32_t s_first;   // the workgroup's first row, when it began in an earlier one
+    __shared__ float s_first_val;
     __shared__ int32_t t_row[kMgThreads], t_flag[2][kMgThreads], t_sf[2][kMgThreads];
     __shared__ float t_val[2][kMgThreads];
     const int tid = threadIdx.x;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     // Heads: the thread finished a row started before it -- join it with the tails before.
     // Only the workgroup's first row can have started in an earlier workgroup; its end part
     // goes to the workgroup's record.
-    if (tid == 0) s_corner[0] = -1;
+    if (tid == 0) s_first = -1;
     __syncthreads();
     if (has_head) {
         float tot = head;
@@ -168,8 +169,8 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
         if (started_here) {
             y[first_row] = tot;
         } else {
-            s_corner[0] = first_row;
-            t_val[cur ^ 1][0] = tot;
+            s_first = first_row;
+            s_first_val = tot;
         }
     }
     // The workgroup's last open row (the thread holding the slice's last item).
@@ -181,8 +182,8 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     }
     __syncthreads();
     if (tid == 0) {
-        rec[blockIdx.x].first_row = s_corner[0];
-        rec[blockIdx.x].first_val = s_corner[0] >= 0 ? t_val[cur ^ 1][0] : 0.0f;
+        rec[blockIdx.x].first_row = s_first;
+        rec[blockIdx.x].first_val = s_first >= 0 ? s_first_val : 0.0f;
     }
 }
 
