@@ -102,6 +102,9 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.d_tiles);
     (void)hipFree(m->plan.d_merge);
     (void)hipFree(m->plan.d_merge_corner);
+    (void)hipFree(m->plan.d_mstage_w);
+    (void)hipFree(m->plan.d_mstage_z);
+    (void)hipFree(m->plan.d_mstage_tab);
     (void)hipFree(m->plan.d_long_rows);
     (void)hipFree(m->plan.d_long_ptr);
     (void)hipFree(m->plan.d_chunks);
@@ -593,6 +596,35 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
     return SM_OK;
 }
 
+// The merge path's column-sorted staging stream (kernels_merge.hip MergeStage), over the
+// columns the merge kernel gathers with (the relabeled ones when the plan has them).
+bool want_merge_stage(const sm_matrix *m) {
+    if (m->nnz <= 0 || m->n_rows <= 0) return false;
+    if (const char *e = dev_env("SM_MERGE_STAGE")) return atoi(e) != 0;
+    return false;
+}
+
+sm_status upload_merge_stage(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    std::vector<int32_t> rcol;
+    if (m->plan.n_relabel > 0) {   // the relabeled columns (the plan keeps them on the device)
+        rcol.resize((size_t)m->nnz);
+        SM_TRY_HIP(hipMemcpy(rcol.data(), m->plan.d_rcol, (size_t)m->nnz * 4, hipMemcpyDeviceToHost));
+        col = rcol.data();
+    }
+    std::vector<uint32_t> w;
+    std::vector<uint16_t> z;
+    std::vector<float> table;
+    if (!merge_stage_build(rp, col, val, m->n_rows, m->n_cols, m->nnz, w, z, table)) return SM_OK;
+    Plan &p = m->plan;
+    SM_TRY_HIP(dev_alloc(&p.d_mstage_w, m->nnz, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_mstage_z, m->nnz, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&p.d_mstage_tab, 256, m->device_bytes));
+    SM_TRY_HIP(hipMemcpy(p.d_mstage_w, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(p.d_mstage_z, z.data(), z.size() * 2, hipMemcpyHostToDevice));
+    SM_TRY_HIP(hipMemcpy(p.d_mstage_tab, table.data(), 256 * 4, hipMemcpyHostToDevice));
+    return SM_OK;
+}
+
 // Sorted sliced-ELL (sell.h, kernels_sell.hip) for every matrix no band layout
 // serves (SM_SELL=0 disables it): faster than the stream kernel on uniform rows
 // (config-2 shape without bands 100 vs 109 us, 2^17 rows 14.5 vs 15.8 us) and on
@@ -1039,6 +1071,7 @@ sm_status finish_from_host_csr(sm_matrix *m, const int32_t *rp, const int32_t *c
     if (st2 == SM_OK && want_relabel_size(m)) st2 = upload_relabel(m, col);
     if (st2 == SM_OK && want_ccsell(m)) st2 = upload_ccsell(m, rp, col, val);
     if (st2 == SM_OK && want_sell(m)) st2 = upload_sell_layouts(m, rp, col, val);
+    if (st2 == SM_OK && want_merge_stage(m)) st2 = upload_merge_stage(m, rp, col, val);
     if (st2 == SM_OK && want_exact_sell(m)) st2 = upload_exact_sell(m, rp, col, val);
     return st2;
 }
@@ -1443,6 +1476,9 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
         if (st == SM_OK && want_ccsell(m.get())) st = upload_ccsell(m.get(), rp.data(), ch.data(), vh.data());
         if (st == SM_OK && want_sell(m.get())) st = values();
         if (st == SM_OK && want_sell(m.get())) st = upload_sell_layouts(m.get(), rp.data(), ch.data(), vh.data());
+        if (st == SM_OK && want_merge_stage(m.get())) st = values();
+        if (st == SM_OK && want_merge_stage(m.get()))
+            st = upload_merge_stage(m.get(), rp.data(), ch.data(), vh.data());
     }
     if (st != SM_OK) { free_device(m.get()); return st; }
     *out = m.release();
@@ -1737,17 +1773,19 @@ sm_status sm_spmv(const sm_matrix *m, float alpha, const float *x, float beta, f
         e = launch_spmv_stream(m->plan, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
                                m->plan.d_partials, s);
         break;
-    case SM_ALGO_MERGE:   // merge path over the CSR arrays (kernels_merge.hip)
+    case SM_ALGO_MERGE: {   // merge path over the CSR arrays (kernels_merge.hip)
+        const MergeStage mstage{m->plan.d_mstage_w, m->plan.d_mstage_z, m->plan.d_mstage_tab};
         if (m->plan.n_relabel > 0) {   // skewed columns: the relabeled copy, hot x in L2 (as stream)
             e = launch_x_relabel(m->plan.n_relabel, m->plan.d_perm, x, m->plan.d_xperm, s);
             if (e == hipSuccess)
                 e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->plan.d_rcol, m->d_val, m->plan.d_xperm, y,
-                                      alpha, beta, m->plan.d_merge_corner, m->plan.d_merge, s);
+                                      alpha, beta, m->plan.d_merge_corner, m->plan.d_merge, s, &mstage);
             break;
         }
         e = launch_spmv_merge(n, (int32_t)m->nnz, m->d_row_ptr, m->d_col, m->d_val, x, y, alpha, beta,
-                              m->plan.d_merge_corner, m->plan.d_merge, s);
+                              m->plan.d_merge_corner, m->plan.d_merge, s, &mstage);
         break;
+    }
     case kAlgoExactSell: {   // unsegmented slices: every row in stored order, one lane each
         const float *xs = x;
         if (m->plan.n_relabel > 0) {   // the slices hold relabeled columns

@@ -23,7 +23,10 @@
 #include "xband_dev.h"
 
 #include <algorithm>
+#include <thread>
 #include <vector>
+
+#include "xband.h"
 
 namespace smamd {
 namespace {
@@ -50,14 +53,19 @@ __device__ __forceinline__ void merge_corner(int64_t d, RendT rend, int64_t n, i
     nz = d - lo;
 }
 
+// STAGE: the slice's terms come from the column-sorted staging stream (MergeStage) instead of
+// the CSR order -- the same terms, the same products, placed at the same LDS slots.
+template <bool STAGE>
 __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     int32_t n, int32_t nnz, const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ x, float *__restrict__ y, float alpha, float beta,
-    const int2 *__restrict__ corner, MergeRec *__restrict__ rec) {
+    const int2 *__restrict__ corner, MergeRec *__restrict__ rec, const uint32_t *__restrict__ sw,
+    const uint16_t *__restrict__ sz, const float *__restrict__ stab) {
     __shared__ float s_term[kMgTile];
     __shared__ int32_t s_rend[kMgTile];
     __shared__ int32_t s_first;   // the workgroup's first row, when it began in an earlier one
     __shared__ float s_first_val;
+    __shared__ float s_tab[STAGE ? 256 : 1];   // fl(table[id] * alpha)
     __shared__ int32_t t_row[kMgThreads], t_flag[2][kMgThreads], t_sf[2][kMgThreads];
     __shared__ float t_val[2][kMgThreads];
     const int tid = threadIdx.x;
@@ -65,7 +73,25 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     const int32_t r0 = c0.x, z0 = c0.y, r1 = c1.x, z1 = c1.y;
     const int32_t tile_rows = r1 - r0, tile_nnz = z1 - z0;
     // Stage: the slice's terms (every load issued before the first is used) and row ends.
-    {
+    if constexpr (STAGE) {
+        s_tab[tid] = __fmul_rn(stab[tid], alpha);
+        uint32_t w[kMgIpt];
+        uint32_t zz[kMgIpt];
+#pragma unroll
+        for (int k = 0; k < kMgIpt; ++k) {
+            const int32_t z = k * kMgThreads + tid;
+            const int32_t gz = z < tile_nnz ? z0 + z : 0;   // nnz > 0 here
+            w[k] = sw[gz];
+            zz[k] = sz[gz];
+        }
+        __syncthreads();   // s_tab
+#pragma unroll
+        for (int k = 0; k < kMgIpt; ++k) {
+            const int32_t z = k * kMgThreads + tid;
+            const float xv = x[w[k] >> 8];
+            if (z < tile_nnz) s_term[zz[k]] = __fmul_rn(xv, s_tab[w[k] & 255u]);
+        }
+    } else {
         int32_t c[kMgIpt];
         float v[kMgIpt];
 #pragma unroll
@@ -81,11 +107,11 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
             const float xv = x[c[k]];
             if (z < tile_nnz) s_term[z] = __fmul_rn(xv, __fmul_rn(v[k], alpha));
         }
+    }
 #pragma unroll
-        for (int k = 0; k < kMgIpt; ++k) {
-            const int32_t r = k * kMgThreads + tid;
-            if (r < tile_rows) s_rend[r] = rp[r0 + 1 + r] - z0;
-        }
+    for (int k = 0; k < kMgIpt; ++k) {
+        const int32_t r = k * kMgThreads + tid;
+        if (r < tile_rows) s_rend[r] = rp[r0 + 1 + r] - z0;
     }
     const int32_t rstart0 = rp[r0] - z0;   // the slice's first row's start (<= 0)
     __syncthreads();
@@ -223,15 +249,51 @@ void merge_corners(const int32_t *rp, int64_t n_rows, int64_t nnz, std::vector<i
     }
 }
 
+bool merge_stage_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows, int64_t n_cols,
+                       int64_t nnz, std::vector<uint32_t> &w, std::vector<uint16_t> &z, std::vector<float> &table) {
+    if (nnz <= 0 || n_cols > (1 << 24)) return false;
+    std::vector<uint8_t> ids;
+    if (!codebook_ids(val, nnz, table, ids)) return false;
+    table.resize(256, 0.0f);
+    std::vector<int32_t> corners;
+    merge_corners(rp, n_rows, nnz, corners);
+    const int64_t nb = (int64_t)corners.size() / 2 - 1;
+    w.resize((size_t)nnz);
+    z.resize((size_t)nnz);
+    const int nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++)
+        th.emplace_back([&, t] {
+            std::vector<int32_t> ord;
+            for (int64_t b = t; b < nb; b += nthr) {
+                const int32_t z0 = corners[(size_t)(2 * b + 1)], z1 = corners[(size_t)(2 * b + 3)];
+                ord.resize((size_t)(z1 - z0));
+                for (int32_t k = 0; k < z1 - z0; k++) ord[(size_t)k] = k;
+                std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t c) { return col[z0 + a] < col[z0 + c]; });
+                for (int32_t k = 0; k < z1 - z0; k++) {
+                    const int32_t e = z0 + ord[(size_t)k];
+                    w[(size_t)(z0 + k)] = ((uint32_t)col[e] << 8) | ids[(size_t)e];
+                    z[(size_t)(z0 + k)] = (uint16_t)ord[(size_t)k];
+                }
+            }
+        });
+    for (auto &x : th) x.join();
+    return true;
+}
+
 hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
                              const float *x, float *y, float alpha, float beta, const int2 *corner, MergeRec *rec,
-                             hipStream_t s) {
+                             hipStream_t s, const MergeStage *stage) {
     if (n <= 0) return hipSuccess;
     if (nnz == 0) return launch_beta(y, 1, n, n, beta, s);
     const int64_t nb = merge_blocks(n, nnz);
     if (nb > INT32_MAX || !rec || !corner) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(spmv_merge_kernel, dim3((unsigned)nb), dim3(kMgThreads), 0, s, n, nnz, rp, col, val, x, y,
-                       alpha, beta, corner, rec);
+    if (stage && stage->w && stage->z && stage->table)
+        hipLaunchKernelGGL(spmv_merge_kernel<true>, dim3((unsigned)nb), dim3(kMgThreads), 0, s, n, nnz, rp, col, val,
+                           x, y, alpha, beta, corner, rec, stage->w, stage->z, stage->table);
+    else
+        hipLaunchKernelGGL(spmv_merge_kernel<false>, dim3((unsigned)nb), dim3(kMgThreads), 0, s, n, nnz, rp, col,
+                           val, x, y, alpha, beta, corner, rec, nullptr, nullptr, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(spmv_merge_fixup_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, (int32_t)nb,

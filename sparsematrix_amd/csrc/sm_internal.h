@@ -180,11 +180,23 @@ struct MergeRec {
     int32_t pad[3];
 };
 int64_t merge_blocks(int64_t n_rows, int64_t nnz);
+// The staging stream on the host: false when it does not apply (values not a <= 255-entry
+// codebook, columns past 2^24).  col: the columns the kernel gathers with (relabeled or not).
+bool merge_stage_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows, int64_t n_cols,
+                       int64_t nnz, std::vector<uint32_t> &w, std::vector<uint16_t> &z, std::vector<float> &table);
 // The (row, term) corner of every workgroup's slice, blocks + 1 of them (x = row, y = term).
 void merge_corners(const int32_t *rp, int64_t n_rows, int64_t nnz, std::vector<int32_t> &out);
+// The merge path's staging stream: every slice's terms in ascending column order, as
+// (column << 8 | codebook id) words and their place in the slice -- so a wave's x gathers
+// hit few cache lines where columns repeat (the hot, relabeled prefix of a skewed graph).
+struct MergeStage {
+    const uint32_t *w = nullptr;   // nnz words, slice by slice at the CSR positions [z0, z1)
+    const uint16_t *z = nullptr;   // nnz positions in the slice (term z0 + z[k] of the CSR)
+    const float *table = nullptr;  // 256 codebook values (0 past the table)
+};
 hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const int32_t *col, const float *val,
                              const float *x, float *y, float alpha, float beta, const int2 *corner, MergeRec *rec,
-                             hipStream_t s);
+                             hipStream_t s, const MergeStage *stage = nullptr);
 
 struct Plan {
     XbandDev xb;                      // n_blocks == 0 when not built
@@ -220,6 +232,9 @@ struct Plan {
     // Merge-path SpMV (kernels_merge.hip): one record per workgroup (one SpMV in flight).
     MergeRec *d_merge = nullptr;
     int2 *d_merge_corner = nullptr;   // merge_blocks + 1 slice corners
+    uint32_t *d_mstage_w = nullptr;   // the merge path's column-sorted staging stream (MergeStage)
+    uint16_t *d_mstage_z = nullptr;
+    float *d_mstage_tab = nullptr;
 };
 
 // Host launchers (kernels.hip).  All return hipError_t of the launch.

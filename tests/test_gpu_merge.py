@@ -126,3 +126,23 @@ def test_merge_edge_shapes(sm):
     want = oracle.csr_spmv(rp0, np.zeros(0, np.int32), np.zeros(0, np.float32), np.ones(100, np.float32),
                            y0, 1.0, 0.25)
     assert np.array_equal(bits(to_host(y)), bits(want))
+
+
+def test_merge_codebook_skewed(sm):
+    """Codebook values (<= 255 distinct) on skewed rows with relabeled columns: where the plan
+    carries the column-sorted staging stream the terms are staged in column order -- the same
+    products in the same LDS slots, so the same bits as the CSR-order staging."""
+    rng = np.random.default_rng(21)
+    n_rows, n_cols = 40000, 1 << 16
+    lens = np.minimum(rng.zipf(1.7, n_rows), 3000).astype(np.int64)
+    rp = np.zeros(n_rows + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    hot = rng.zipf(1.5, int(rp[-1])) % n_cols            # skewed column degrees
+    ci = np.concatenate([np.unique(np.concatenate([hot[rp[r]:rp[r + 1]], [r % n_cols]]))[:lens[r]]
+                         for r in range(n_rows)]).astype(np.int32)
+    lens = np.array([min(len(np.unique(np.concatenate([hot[rp[r]:rp[r + 1]], [r % n_cols]]))), lens[r])
+                     for r in range(n_rows)], np.int64)
+    rp[1:] = np.cumsum(lens)
+    table = rng.uniform(-1, 1, 200).astype(np.float32)
+    va = table[rng.integers(0, 200, ci.size)]
+    _check(sm, rp.astype(np.int32), ci, va, n_cols, 1.3, 0.5, seed=22)
