@@ -134,15 +134,11 @@ def test_merge_codebook_skewed(sm):
     products in the same LDS slots, so the same bits as the CSR-order staging."""
     rng = np.random.default_rng(21)
     n_rows, n_cols = 40000, 1 << 16
-    lens = np.minimum(rng.zipf(1.7, n_rows), 3000).astype(np.int64)
+    lens = np.minimum(rng.zipf(1.7, n_rows), 3000)
+    rows = [np.unique(rng.zipf(1.5, int(k)) % n_cols) for k in lens]   # skewed column degrees
     rp = np.zeros(n_rows + 1, np.int64)
-    rp[1:] = np.cumsum(lens)
-    hot = rng.zipf(1.5, int(rp[-1])) % n_cols            # skewed column degrees
-    ci = np.concatenate([np.unique(np.concatenate([hot[rp[r]:rp[r + 1]], [r % n_cols]]))[:lens[r]]
-                         for r in range(n_rows)]).astype(np.int32)
-    lens = np.array([min(len(np.unique(np.concatenate([hot[rp[r]:rp[r + 1]], [r % n_cols]]))), lens[r])
-                     for r in range(n_rows)], np.int64)
-    rp[1:] = np.cumsum(lens)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    ci = np.concatenate(rows).astype(np.int32)
     table = rng.uniform(-1, 1, 200).astype(np.float32)
     va = table[rng.integers(0, 200, ci.size)]
     _check(sm, rp.astype(np.int32), ci, va, n_cols, 1.3, 0.5, seed=22)
