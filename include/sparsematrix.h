@@ -150,6 +150,8 @@ typedef struct sm_info {
     int32_t xband_slab0_cols;   /* columns of slab 0 (slab s >= 1 covers [slab0 + (s-1) *
                                    xband_slab_cols, slab0 + s * xband_slab_cols)); equal to
                                    xband_slab_cols when the slabs are even                  */
+    int32_t merge_stage;        /* 1: SM_ALGO_MERGE stages terms from the column-sorted copy
+                                   (sm_build_opts.merge_stage)                               */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */
@@ -252,6 +254,11 @@ typedef struct sm_build_opts {
                                   share of an even split, in permille (0 = auto = 1000, even
                                   slabs); the other slabs share the rest evenly.  The slab-0
                                   tile also loads and scales y before its first band        */
+    int32_t merge_stage;       /* SM_ALGO_MERGE on skewed graphs: 1 builds a column-sorted copy of
+                                  each merge tile's terms (4-byte column | codebook-id words and
+                                  2-byte slots, 6 bytes per term) when the values form a codebook
+                                  and n_cols <= 2^24; the tile gathers x in column order (R-MAT 24:
+                                  1.91 -> 1.68 ms), same bits as without.  0 = never (default)  */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);

@@ -77,6 +77,7 @@ class SmInfo(C.Structure):
         ("sell_slices", C.c_int64), ("sell_codebook", C.c_int32), ("ccsell_chunks", C.c_int32),
         ("hot_cols", C.c_int32), ("sweep_blocks", C.c_int32),
         ("exact_sell_slices", C.c_int64), ("exact_algo", C.c_int32), ("xband_slab0_cols", C.c_int32),
+        ("merge_stage", C.c_int32),
     ]
 
 
@@ -92,7 +93,7 @@ class SmBuildOpts(C.Structure):
         ("sell_codebook", C.c_int32), ("sell_max_len", C.c_int32), ("sell_streams", C.c_int32),
         ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
         ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32), ("hot_cols", C.c_int32),
-        ("exact_sell", C.c_int32), ("band_slab0_permille", C.c_int32),
+        ("exact_sell", C.c_int32), ("band_slab0_permille", C.c_int32), ("merge_stage", C.c_int32),
     ]
 
 

@@ -191,6 +191,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.hot_cols = d.hot_cols;
         r.exact_sell = d.exact_sell;
         r.band_slab0_permille = d.band_slab0_permille;
+        r.merge_stage = d.merge_stage;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -214,6 +215,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     if (const char *e = dev_env("SM_CCSELL")) r.ccsell = atoi(e);
     if (const char *e = dev_env("SM_CCSELL_CHUNK")) r.ccsell_chunk_log2 = atoi(e);
     if (const char *e = dev_env("SM_HOT_COLS")) r.hot_cols = atoi(e);
+    if (const char *e = dev_env("SM_MERGE_STAGE")) r.merge_stage = atoi(e);
     return r;
 }
 
@@ -241,6 +243,7 @@ sm_status check_opts(const sm_build_opts *o) {
     if (r.exact_sell < -1 || r.exact_sell > 1) return fail(SM_ERR_INVALID_ARG, "exact_sell must be -1, 0 or 1");
     if (r.band_slab0_permille != 0 && (r.band_slab0_permille < 500 || r.band_slab0_permille > 1000))
         return fail(SM_ERR_INVALID_ARG, "band_slab0_permille must be 0 or 500..1000");
+    if (r.merge_stage != 0 && r.merge_stage != 1) return fail(SM_ERR_INVALID_ARG, "merge_stage must be 0 or 1");
     return SM_OK;
 }
 
@@ -599,9 +602,7 @@ sm_status upload_relabel(sm_matrix *m, const int32_t *col) {
 // The merge path's column-sorted staging stream (kernels_merge.hip MergeStage), over the
 // columns the merge kernel gathers with (the relabeled ones when the plan has them).
 bool want_merge_stage(const sm_matrix *m) {
-    if (m->nnz <= 0 || m->n_rows <= 0) return false;
-    if (const char *e = dev_env("SM_MERGE_STAGE")) return atoi(e) != 0;
-    return false;
+    return m->nnz > 0 && m->n_rows > 0 && m->opts.merge_stage == 1;
 }
 
 sm_status upload_merge_stage(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
@@ -1534,6 +1535,7 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
             ? m->plan.xb.slab_bands   // band2 / cband / gcb keep slab columns there
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->xband_slab0_cols = m->plan.xb.slab0_cols > 0 ? m->plan.xb.slab0_cols : info->xband_slab_cols;
+    info->merge_stage = m->plan.d_mstage_w ? 1 : 0;
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;

@@ -54,6 +54,7 @@ struct BuildOpts {
     int32_t hot_cols = 0;
     int32_t exact_sell = 0;   // 0 auto, 1 always, -1 never (sm_build_opts.exact_sell)
     int32_t band_slab0_permille = 0;   // 0 auto (sm_build_opts.band_slab0_permille)
+    int32_t merge_stage = 0;           // sm_build_opts.merge_stage
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile

@@ -87,6 +87,12 @@ def test_argument_validation_without_gpu(lib):
     assert lib.sm_create_from_csr(2, 4, 1, bad_rp.ctypes.data, ci.ctypes.data, va.ctypes.data, 0,
                                   C.byref(h)) == 6
     assert lib.sm_spmv(None, 1.0, None, 1.0, None, 0, None) == 1
+    from sparsematrix_amd import _lib
+    rp = np.array([0, 1], np.int32)
+    for bad in (dict(merge_stage=2), dict(band_tall=5), dict(layout=42)):
+        o = _lib.build_opts(**bad)
+        assert lib.sm_create_from_csr_ex(1, 4, 1, rp.ctypes.data, ci.ctypes.data, va.ctypes.data, 0,
+                                         C.byref(o), C.byref(h)) == 1, bad
 
 
 def test_python_mirror_surface():
@@ -110,17 +116,17 @@ def test_header_and_python_mirror_agree():
     for name, val in _lib.ALGOS.items():
         m = re.search(r"SM_ALGO_%s\s*=\s*(\d+)" % name.upper(), hdr)
         assert m and int(m.group(1)) == val, name
-    src = ('#include <stddef.h>\n#include <stdio.h>\n#include "sparsematrix.h"\n'
-           'int main(void){printf("%zu %zu %zu\\n", sizeof(sm_info), offsetof(sm_info, sell_slices),'
-           ' offsetof(sm_info, sell_codebook));'
-           'return 0;}\n')
+    structs = (("sm_info", _lib.SmInfo), ("sm_build_opts", _lib.SmBuildOpts))
+    body = "".join('printf("%%zu\\n", sizeof(%s));' % c + "".join(
+        'printf("%%zu\\n", offsetof(%s, %s));' % (c, f) for f, _ in py._fields_) for c, py in structs)
+    src = '#include <stddef.h>\n#include <stdio.h>\n#include "sparsematrix.h"\nint main(void){%sreturn 0;}\n' % body
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
         open(c, "w").write(src)
         exe = os.path.join(d, "t")
         subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
-        size, off, off_cb = map(int, subprocess.run([exe], capture_output=True, text=True,
-                                                    check=True).stdout.split())
-    assert ctypes.sizeof(_lib.SmInfo) == size
-    assert _lib.SmInfo.sell_slices.offset == off
-    assert _lib.SmInfo.sell_codebook.offset == off_cb
+        got = iter(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
+    for cname, py in structs:   # every field of the ctypes mirror at the header's offset
+        assert ctypes.sizeof(py) == next(got), cname
+        for f, _ in py._fields_:
+            assert getattr(py, f).offset == next(got), (cname, f)

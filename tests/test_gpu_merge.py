@@ -4,6 +4,8 @@ every thread 8, so rows are cut anywhere.  A row whose items all fall in one thr
 summed in stored order from beta*y -- bit-identical to the reference
 (/root/reference/src/sparse/kernel.cc:780-796, :791 for the term); cut rows join their parts
 in a fixed order: within 1e-6 * sum|terms| of the reference, and deterministic."""
+import os
+
 import numpy as np
 import pytest
 
@@ -12,7 +14,9 @@ from gpu_util import assert_terms_close, bits, to_dev, to_host, torch_dev, unifo
 
 pytestmark = pytest.mark.gpu
 
-IPT, TILE = 8, 2048   # merge items per thread / per workgroup (kernels_merge.hip)
+# merge items per thread (kernels_merge.hip SM_MERGE_IPT; development builds with another value
+# set it here too, tools/r5_merge_ipt.sh)
+IPT = int(os.environ.get("SM_MERGE_IPT", "8"))
 
 
 @pytest.fixture(scope="module")
@@ -32,8 +36,9 @@ def _one_thread_rows(rp):
     return (start // IPT) == (end // IPT)
 
 
-def _check(sm, rp, ci, va, n_cols, alpha, beta, seed, y_special=False):
-    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+def _check(sm, rp, ci, va, n_cols, alpha, beta, seed, y_special=False, want_stage=None):
+    """Both plans -- without and with the column-sorted staging copy (sm_build_opts.merge_stage,
+    built only for codebook values) -- against the oracle, and against each other bit for bit."""
     rng = np.random.default_rng(seed)
     x = rng.uniform(-1, 1, n_cols).astype(np.float32)
     y0 = rng.uniform(-1, 1, rp.size - 1).astype(np.float32)
@@ -41,12 +46,17 @@ def _check(sm, rp, ci, va, n_cols, alpha, beta, seed, y_special=False):
         y0[::101] = np.nan
         y0[1::103] = -0.0
     outs = []
-    for _ in range(2):
-        y = to_dev(y0)
-        M.spmv(to_dev(x), y, alpha, beta, algo="merge")
-        outs.append(to_host(y))
+    for stage in (0, 1):
+        M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts={"merge_stage": stage})
+        if stage and want_stage is not None:
+            assert M.info()["merge_stage"] == want_stage
+        for _ in range(2):
+            y = to_dev(y0)
+            M.spmv(to_dev(x), y, alpha, beta, algo="merge")
+            outs.append(to_host(y))
     got = outs[0]
-    assert np.array_equal(bits(outs[0]), bits(outs[1])), "not deterministic"
+    for o in outs[1:]:
+        assert np.array_equal(bits(got), bits(o)), "not deterministic, or the staging copy changed bits"
     want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     one = _one_thread_rows(rp)
     assert np.array_equal(bits(got[one]), bits(want[one])), "rows inside one thread must be bit-exact"
@@ -129,9 +139,9 @@ def test_merge_edge_shapes(sm):
 
 
 def test_merge_codebook_skewed(sm):
-    """Codebook values (<= 255 distinct) on skewed rows with relabeled columns: where the plan
-    carries the column-sorted staging stream the terms are staged in column order -- the same
-    products in the same LDS slots, so the same bits as the CSR-order staging."""
+    """Codebook values (<= 255 distinct) on skewed rows with relabeled columns: with
+    sm_build_opts.merge_stage the terms are staged in column order -- the same products in the
+    same LDS slots, so the same bits as the CSR-order staging."""
     rng = np.random.default_rng(21)
     n_rows, n_cols = 40000, 1 << 16
     lens = np.minimum(rng.zipf(1.7, n_rows), 3000)
@@ -141,4 +151,7 @@ def test_merge_codebook_skewed(sm):
     ci = np.concatenate(rows).astype(np.int32)
     table = rng.uniform(-1, 1, 200).astype(np.float32)
     va = table[rng.integers(0, 200, ci.size)]
-    _check(sm, rp.astype(np.int32), ci, va, n_cols, 1.3, 0.5, seed=22)
+    _check(sm, rp.astype(np.int32), ci, va, n_cols, 1.3, 0.5, seed=22, want_stage=1)
+    # values beyond a codebook: the option is accepted and nothing is built
+    va2 = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    _check(sm, rp.astype(np.int32), ci, va2, n_cols, 1.0, 0.0, seed=23, want_stage=0)

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--algos", default="xband,vector,parity")
     ap.add_argument("--json", default="")
     ap.add_argument("--ablate", default="", help="xband ablation modes (dev), e.g. 1,2,4")
+    ap.add_argument("--opts", default="{}", help='sm_build_opts for the --algos matrices, JSON, '
+                    'e.g. \'{"merge_stage": 1}\'')
     args = ap.parse_args()
 
     import torch
@@ -86,7 +88,8 @@ def main():
     for a in [int(v) for v in args.ablate.split(",") if v]:
         variants.append((f"xband/ablate{a}", ("xband", a), xmats))
     os.environ["SM_XBAND"] = "0"
-    base_mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc) for rp, ci, va, nc, _, _ in data]
+    base_mats = [smd.SparseMatrix.from_csr(rp, ci, va, nc, opts=json.loads(args.opts))
+                 for rp, ci, va, nc, _, _ in data]
     os.environ.pop("SM_XBAND")
     for a in [a for a in args.algos.split(",") if a and a not in ("xband", "exact")]:
         variants.append((a, a, base_mats))
