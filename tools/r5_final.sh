@@ -1,13 +1,14 @@
 #!/bin/bash
 # Round-5 record run: the GPU test suite, the default bench line, rocprofv3 kernel stats of
-# the bench's config-2 run, and the PMC traffic passes (tools/pmc.sh).  Stops at the first
+# the bench's config-2 run, the PMC traffic passes (tools/pmc.sh) and the 2-rank rehearsal of
+# the N > 1 bookkeeping (SM_BENCH_REHEARSE, both ranks on GPU 0).  Stops at the first
 # crash / time limit.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
-STEPS=${STEPS:-tests,bench,stats,pmc}
+STEPS=${STEPS:-tests,bench,stats,pmc,rehearse}
 if [[ ,$STEPS, == *,tests,* ]]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > "$OUT/r5f_tests.log" 2>&1
   rc=$?; tail -4 "$OUT/r5f_tests.log"; echo "tests rc=$rc"
@@ -30,5 +31,9 @@ if [[ ,$STEPS, == *,stats,* ]]; then
 fi
 if [[ ,$STEPS, == *,pmc,* ]]; then
   BENCH_ARGS="--no-config5 --no-fp32-values" bash tools/pmc.sh || exit $?
+fi
+if [[ ,$STEPS, == *,rehearse,* ]]; then
+  SM_BENCH_REHEARSE=1 timeout -k 10 400 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu --no-spmm --no-rmat > "$OUT/r5f_rehearse.log" 2>&1 || { tail -20 "$OUT/r5f_rehearse.log"; exit 33; }
+  grep '^{' "$OUT/r5f_rehearse.log" | tail -1 > "$OUT/r5f_rehearse_line.json"; cut -c1-300 "$OUT/r5f_rehearse_line.json"
 fi
 echo "r5_final done"
