@@ -15,7 +15,7 @@ from gpu_util import assert_terms_close, bits, to_dev, to_host, torch_dev, unifo
 pytestmark = pytest.mark.gpu
 
 # merge items per thread (kernels_merge.hip SM_MERGE_IPT; development builds with another value
-# set it here too, tools/r5_merge_ipt.sh)
+# set it here too, tools/archive/r5_merge_ipt2.sh)
 IPT = int(os.environ.get("SM_MERGE_IPT", "8"))
 
 
