@@ -42,7 +42,8 @@ Also on the same JSON line:
                 config 1 and 16k^2; and R-MAT over all cores.  ~30 s of CPU work.
   spmm          config 3 (same matrix, N = 32 right-hand sides): GFLOP/s, HBM fraction,
                 traffic and MFMA utilisation from PMC (profiles/), median of 20.
-  rmat          config 4 (R-MAT scale 24) SpMV, median of 20.
+  rmat          config 4 (R-MAT scale 24) SpMV, median of 20; merge_path: the same matrix by
+                SM_ALGO_MERGE, over the CSR arrays and with its staging copy.
 """
 from __future__ import annotations
 
@@ -559,6 +560,27 @@ def main():
                     "generate_s": round(t_g - t_b, 1), "build_s": round(t_c - t_g, 1),
                     "timing": "HIP events around each SpMV (median of 20 eager launches, x "
                               "permutation and finalize included)"}
+            # north_star's merge-path row balancing (SM_ALGO_MERGE) on the same
+            # matrix: over the CSR arrays, then with its column-sorted staging copy
+            try:
+                m_list = event_times(torch, lambda i: RM.spmv(rx, ry, 1.0, 0.5, algo="merge"), 20)
+                t_m = time.perf_counter()
+                RS = smd.SparseMatrix.from_csr(rrp, rci, rva, rn, device=dev_index, opts={"merge_stage": 1})
+                ms_build = time.perf_counter() - t_m
+                for _ in range(3):
+                    RS.spmv(rx, ry, 1.0, 0.5, algo="merge")
+                s_list = event_times(torch, lambda i: RS.spmv(rx, ry, 1.0, 0.5, algo="merge"), 20)
+                m_ms, s_ms = float(np.median(m_list)), float(np.median(s_list))
+                rmat["merge_path"] = {
+                    "ms": round(m_ms, 4), "frac": round(rb / (m_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "staged_ms": round(s_ms, 4),
+                    "staged_frac": round(rb / (s_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "merge_stage_built": RS.info()["merge_stage"], "staged_build_s": round(ms_build, 1),
+                    "note": "SM_ALGO_MERGE, median of 20 eager launches; staged = sm_build_opts."
+                            "merge_stage (terms gathered in column order per 2048-item slice)"}
+                del RS
+            except Exception as exc:  # noqa: BLE001
+                rmat["merge_path"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
             if not args.no_cpu:
                 rmat_host = (rrp.cpu().numpy(), rci.cpu().numpy(), rva.cpu().numpy(),
                              rx.cpu().numpy(), ry.cpu().numpy(), rb)
