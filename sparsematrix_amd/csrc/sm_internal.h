@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "sparsematrix.h"
+#include "merge.h"
 
 namespace smamd {
 
@@ -180,13 +181,6 @@ struct MergeRec {
     int32_t last_fresh;
     int32_t pad[3];
 };
-int64_t merge_blocks(int64_t n_rows, int64_t nnz);
-// The staging stream on the host: false when it does not apply (values not a <= 255-entry
-// codebook, columns past 2^24).  col: the columns the kernel gathers with (relabeled or not).
-bool merge_stage_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows, int64_t n_cols,
-                       int64_t nnz, std::vector<uint32_t> &w, std::vector<uint16_t> &z, std::vector<float> &table);
-// The (row, term) corner of every workgroup's slice, blocks + 1 of them (x = row, y = term).
-void merge_corners(const int32_t *rp, int64_t n_rows, int64_t nnz, std::vector<int32_t> &out);
 // The merge path's staging stream: every slice's terms in ascending column order, as
 // (column << 8 | codebook id) words and their place in the slice -- so a wave's x gathers
 // hit few cache lines where columns repeat (the hot, relabeled prefix of a skewed graph).

@@ -123,3 +123,21 @@ def test_gcb_builder_under_asan(tmp_path):
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gcb_asan: ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_merge_plan_under_asan(tmp_path):
+    """Merge path's plan (merge.cpp): slice corners against a sequential walk of the merge,
+    and the column-sorted staging stream (a per-slice permutation, ascending columns with ties
+    in CSR order, codebook ids back to the values' bits; declined past 255 values / 2^24 cols)."""
+    exe = tmp_path / "merge_asan"
+    src = [os.path.join(ROOT, "tests", "native", "merge_asan.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "merge.cpp"),
+           os.path.join(ROOT, "sparsematrix_amd", "csrc", "band2.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-omit-frame-pointer", "-I", os.path.join(ROOT, "sparsematrix_amd", "csrc"),
+                    *src, "-o", str(exe), "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "merge_asan: ok" in r.stdout
