@@ -472,6 +472,15 @@ def main():
                                  if use_graph else "median of per-launch HIP events"),
             "alg_bytes_per_launch": bytes_rank, "distribution": dist_info}
 
+    # ---- config 2 with arbitrary fp32 values (rank 0, N = 1), right after the headline, in
+    # the same chip state (after the R-MAT leg it measured 3 us slower) ----
+    if (world == 1 and emu == 1 and args.workload == "config2" and not args.no_fp32_values
+            and reps[0]["rp"] is not None):
+        try:
+            roof["fp32_values"] = fp32_values_line(args, torch, reps, R, C, bytes_rank, dev, dev_index)
+        except Exception as exc:  # noqa: BLE001
+            roof["fp32_values"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
     # ---- SpMM (config 3) on replica 0 -----------------------------------------------
     spmm = None
     if not args.no_spmm and args.workload == "config2":
@@ -589,13 +598,18 @@ def main():
         except Exception as exc:  # noqa: BLE001
             rmat = {"error": f"{type(exc).__name__}: {exc}"[:300]}
 
-    # ---- config 2 with arbitrary fp32 values (rank 0, N = 1) ------------------------
-    if (world == 1 and emu == 1 and args.workload == "config2" and not args.no_fp32_values
-            and reps[0]["rp"] is not None):
-        try:
-            roof["fp32_values"] = fp32_values_line(args, torch, reps, R, C, bytes_rank, dev, dev_index)
-        except Exception as exc:  # noqa: BLE001
-            roof["fp32_values"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    # ---- the headline's graph again, after the SpMM and R-MAT legs (how
+    # much the chip's state after those legs moves a graph replay of the same SpMVs) ----------
+    if use_graph and (spmm is not None or rmat is not None):
+        again = []
+        for _ in range(max(3, args.replays)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            graph.replay()
+            b.record()
+            torch.cuda.synchronize()
+            again.append(a.elapsed_time(b) / args.steps)
+        roof["replay_after_legs_ms"] = stats(again)
 
     # ---- config 5: 2^26 x 2^26 strong scaling over the job's ranks ------------------
     config5 = None

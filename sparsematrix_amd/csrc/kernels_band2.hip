@@ -50,7 +50,10 @@ constexpr int kB2Threads = 1024;
 __device__ unsigned long long g_b2_prof[8];
 // PROF 2 (SM_BAND2_PROF=2): wall clock (s_memrealtime, 100 MHz) of every tile's start, loop
 // end and finish, from thread 0.
-__device__ unsigned long long g_b2_ts[3 * 4096];
+// PROF 2 also stamps the hand-off (xband_dev.h slab_handoff_epoch): [3] published and drained,
+// [4] arrival add returned, [5] every sibling seen, [6] combine stores drained.
+constexpr int kTs = 8;
+__device__ unsigned long long g_b2_ts[kTs * 4096];
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
-    int32_t *__restrict__ ctl, float alpha, float beta) {
+    int32_t *__restrict__ ctl, float alpha, float beta, int32_t comb) {
     static_assert(GEO == 0 || GEO == 4, "wide or dma3");
     constexpr bool kLd = GEO == 4;   // dma3: wave kLdWave stages x, the others apply
     constexpr B2Geom G = kLd ? (CB ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
 #ifdef SM_DEV
     if constexpr (PROF == 2) {
-        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x] = wall_clock64();
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[kTs * blockIdx.x] = wall_clock64();
     }
 #endif
     [[maybe_unused]] unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -377,12 +380,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         const int id = tid / (kTabCopies / kPer);   // one entry per thread
         tab_v = id < table_size ? table[id] : 0.0f;
     }
-    // Accumulators: beta*y (slab 0) or -0.0 (the identity of fp32 addition: a row without
-    // terms in this slab keeps the sign of a zero y), all loads in flight.
+    // Accumulators: beta*y (slab 0 of a one-slab layout, or of any layout without SM_B2_BL) or
+    // -0.0 (the identity of fp32 addition: a row without terms in this slab keeps the sign of a
+    // zero y), all loads in flight.
     constexpr int kQ = BROWS / (4 * kB2Threads);
     const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
+    const bool y_first = slab == 0 && (n_slabs == 1 || (!SM_B2_BL && !comb));
     float4 yv[kQ];
-    if (slab == 0) {
+    if (y_first) {
         const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
@@ -414,7 +419,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
                 *reinterpret_cast<float4 *>(&tab[kPer * tid + j]) = make_float4(v, v, v, v);
         }
     }
-    if (slab == 0) {
+    if (y_first) {
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             if (beta != 1.0f)
@@ -506,14 +511,14 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
 #ifdef SM_DEV
     if constexpr (PROF == 2) {
-        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x + 1] = wall_clock64();
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[kTs * blockIdx.x + 1] = wall_clock64();
     }
 #endif
 
     auto flush_prof = [&]() {
 #ifdef SM_DEV
         if constexpr (PROF == 2) {
-            if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[3 * blockIdx.x + 2] = wall_clock64();
+            if (threadIdx.x == 0 && blockIdx.x < 4096) g_b2_ts[kTs * blockIdx.x + 2] = wall_clock64();
         }
         if constexpr (PROF == 1) {   // [6] bands, [7] applying waves (the loader adds 1 << 32)
             ph[6] = (unsigned long long)nb;
@@ -536,8 +541,19 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     }
     __syncthreads();   // every wave is past its last x read: the hand-off words live there
     int32_t *s_word = reinterpret_cast<int32_t *>(&xs[0][0]);
-    slab_handoff_epoch<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0,
-                                   nr, slab, n_slabs, y_vec, old_started, snap);
+    unsigned long long *ts = nullptr;
+#ifdef SM_DEV
+    if constexpr (PROF == 2) {
+        if (blockIdx.x < 4096) ts = &g_b2_ts[kTs * blockIdx.x + 3];
+    }
+#endif
+    if (comb)
+        slab_handoff_comb<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0, nr,
+                                      slab, n_slabs, b2_combiner(b, n_slabs), y_vec, old_started, snap, beta, ts);
+    else
+        slab_handoff_epoch<kB2Threads, SM_B2_BL != 0>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials,
+                                                      n_rows, r0, nr, slab, n_slabs, y_vec, old_started, snap,
+                                                      beta, ts);
     flush_prof();
 }
 
@@ -549,7 +565,7 @@ hipError_t launch_prof(int prof, dim3 grid, hipStream_t s, const XbandDev &xb, i
 #define SM_B2P(P)                                                                                   \
     hipLaunchKernelGGL((spmv_band2_kernel<true, GEO, P>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols, \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.comb)
     if (prof == 1) {
         if (GEO != 4) return hipErrorInvalidValue;
         unsigned long long h[8] = {};
@@ -568,21 +584,31 @@ hipError_t launch_prof(int prof, dim3 grid, hipStream_t s, const XbandDev &xb, i
         return hipGetLastError();
     }
     const int nt = (int)std::min<int64_t>(grid.x, 4096);
-    std::vector<unsigned long long> h((size_t)3 * nt);
+    std::vector<unsigned long long> h((size_t)kTs * nt);
     void *sym = nullptr;
     if (hipGetSymbolAddress(&sym, HIP_SYMBOL(g_b2_ts)) != hipSuccess) return hipErrorInvalidValue;
+    (void)hipMemsetAsync(sym, 0, h.size() * 8, s);
     SM_B2P(2);
 #undef SM_B2P
     (void)hipMemcpyAsync(h.data(), sym, h.size() * 8, hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     unsigned long long t0 = ~0ull;
-    for (int i = 0; i < nt; i++) t0 = std::min(t0, h[3 * i]);
-    std::vector<double> st(nt), lp(nt), ep(nt), en(nt);
+    for (int i = 0; i < nt; i++) t0 = std::min(t0, h[kTs * i]);
+    // us (100 MHz): start, loop, epilogue, end; the hand-off's phases where it ran (several slabs)
+    std::vector<double> st(nt), lp(nt), ep(nt), en(nt), pb(nt), ad(nt), pl(nt), cb(nt);
+    const bool ho = xb.n_slabs > 1;
     for (int i = 0; i < nt; i++) {
-        st[i] = (h[3 * i] - t0) * 0.01;   // us (100 MHz)
-        lp[i] = (h[3 * i + 1] - h[3 * i]) * 0.01;
-        ep[i] = (h[3 * i + 2] - h[3 * i + 1]) * 0.01;
-        en[i] = (h[3 * i + 2] - t0) * 0.01;
+        const unsigned long long *u = &h[(size_t)kTs * i];
+        st[i] = (u[0] - t0) * 0.01;
+        lp[i] = (u[1] - u[0]) * 0.01;
+        ep[i] = (u[2] - u[1]) * 0.01;
+        en[i] = (u[2] - t0) * 0.01;
+        if (ho) {
+            pb[i] = (u[3] - u[1]) * 0.01;
+            ad[i] = (u[4] - u[3]) * 0.01;
+            pl[i] = (u[5] - u[4]) * 0.01;
+            cb[i] = (u[6] - u[5]) * 0.01;
+        }
     }
     auto pr = [](const char *nm, std::vector<double> v) {
         std::sort(v.begin(), v.end());
@@ -594,10 +620,17 @@ hipError_t launch_prof(int prof, dim3 grid, hipStream_t s, const XbandDev &xb, i
     pr("start", st);
     pr("loop", lp);
     pr("epilogue", ep);
+    if (ho) {
+        pr(" publish", pb);
+        pr(" add", ad);
+        pr(" wait", pl);
+        pr(" combine", cb);
+    }
     pr("end", en);
     if (dev_env("SM_B2_TS_DUMP")) {
         for (int i = 0; i < nt; i++)
-            fprintf(stderr, "  tile %4d start %6.2f loop %6.2f epi %6.2f\n", i, st[i], lp[i], ep[i]);
+            fprintf(stderr, "  tile %4d start %6.2f loop %6.2f epi %6.2f pub %6.2f add %6.2f wait %6.2f comb %6.2f\n",
+                    i, st[i], lp[i], ep[i], pb[i], ad[i], pl[i], cb[i]);
     }
     return hipGetLastError();
 }
@@ -631,7 +664,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
 #define SM_B2(C, T)                                                                                 \
     hipLaunchKernelGGL((spmv_band2_kernel<C, T, 0>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.comb)
     if (dma3) {
         if (cb) SM_B2(true, 4); else SM_B2(false, 4);
     } else {

@@ -4,6 +4,21 @@
 #include <cstdint>
 #include <vector>
 
+// Beta-last slab hand-off of the band2 / cband kernels (xband_dev.h combine_rows_bl): with
+// several slabs every slab tile sums from -0.0 and the combine forms beta*y, so no tile loads y
+// before its band loop (slab 0's 64 KiB y load made its loop 1.2 us longer than its siblings',
+// r05 tile timeline).  y = (((beta*y + P_0) + P_1) + ...) + P_{S-1}; 0 restores slab 0 starting
+// from beta*y (development A/B only).
+#ifndef SM_B2_BL
+#define SM_B2_BL 1
+#endif
+
+#ifdef __HIPCC__
+#define SM_HD __host__ __device__
+#else
+#define SM_HD
+#endif
+
 namespace smamd {
 
 // Entry word: bits [0, C) column in band, [C, C+K) rank inside the row's segment
@@ -134,6 +149,9 @@ struct Band2Host {
     B2Geom geom = kB2Wide;
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
     int32_t slab0_cols = 0;              // slab 0 = [0, slab0_cols), slab s >= 1 = [slab0 + (s-1) slab_cols, ...)
+    // Combiner tiles (comb_permille >= 1000): slab s of block b = [slab_lo(b, s), slab_lo(b, s + 1)),
+    // the combiner's slab comb_cols wide, the others slab_cols (the last one clipped).
+    int32_t comb_permille = 0, comb_cols = 0;
     int32_t max_bands_per_tile = 0;
     int64_t n_bands = 0;                 // over all tiles
     std::vector<int32_t> tile_band_start;   // n_blocks * n_slabs + 1 (tile t = b * S + s)
@@ -141,6 +159,16 @@ struct Band2Host {
     std::vector<uint32_t> ent;              // 4096 per band
     int64_t real_terms = 0;                 // for the padding report
 };
+
+// Combiner-tile hand-off (band2 / cband with several slabs, comb_permille >= 1000): in row block
+// b the slab tile b2_combiner(b, S) combines the whole block.  Its slab is comb_permille / 1000
+// of an even share wide and the other S - 1 slabs split the rest, so those end their band loops
+// first, publish all their sums (write-through) and leave; the combiner, ending last, adds
+// beta*y and the S slab sums in slab order for every row of the block itself -- after its loop
+// only the poll of the arrival word and the loads of the others' sums, no publish and no
+// second round trip.  (b >> 1) spreads the combiners over all 8 XCDs when S = 4 (blocks 2k and
+// 2k + 1 sit on opposite XCD halves under round-robin dispatch; speed only, never correctness).
+SM_HD inline int32_t b2_combiner(int64_t b, int32_t n_slabs) { return (int32_t)((b >> 1) % n_slabs); }
 
 // Returns false when the layout does not apply: unsorted columns or size limits
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
@@ -151,7 +179,7 @@ struct Band2Host {
 constexpr int32_t kB2Slab0Permille = 1000;
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
-                 B2Geom geom = kB2Wide, int32_t slab0_permille = 1000);
+                 B2Geom geom = kB2Wide, int32_t slab0_permille = 1000, int32_t comb_permille = 0);
 
 // A row's run of terms inside one chunk: row in block, first term index, count.
 struct B2Seg {

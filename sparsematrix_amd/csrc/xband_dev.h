@@ -138,6 +138,62 @@ __device__ __forceinline__ void combine_rows(const float *yacc, float *y, const 
     }
 }
 
+// Beta-last form (band2 / cband with several slabs): every slab tile sums from -0.0 and
+// publishes into partials[s]; y[lo, hi) = (((beta*y + P_0) + P_1) + ...) + P_{S-1}, beta*y
+// formed here (kernel.cc:10-29: y *= beta unless beta == 1).  y is read by plain loads: in
+// this form no tile writes a y row it does not combine itself.
+template <int THREADS>
+__device__ __forceinline__ void combine_rows_bl(const float *yacc, float *y, const float *partials,
+                                                int64_t ps, int32_t r0, int32_t nr, int32_t me,
+                                                int32_t n_slabs, bool y_vec, float beta, int32_t lo,
+                                                int32_t hi) {
+    if (lo >= hi) return;
+    const int32_t tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
+    auto src = [&](int32_t s) { return rsrc(partials + (int64_t)s * ps + r0, (uint64_t)nr * 4); };
+    auto bop = [&](float v) { return beta != 1.0f ? __fmul_rn(v, beta) : v; };
+    const int32_t hv = y_vec ? lo + ((hi - lo) & ~3) : lo;
+    for (int32_t i = lo + 4 * tid; i < hv; i += 4 * THREADS) {
+        const u32x4 yu = __builtin_amdgcn_raw_buffer_load_b128(y_src, 4u * (uint32_t)i, 0, 0);
+        const float4 own = *reinterpret_cast<const float4 *>(&yacc[i]);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int32_t s0 = 0; s0 < n_slabs; s0 += 4) {
+            u32x4 pv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // the own slab's part and slots past S: no request
+                const int32_t s = min(s0 + j, n_slabs - 1);
+                const uint32_t off = (s == me || s0 + j >= n_slabs) ? 0xFFFFFFF0u : 4u * (uint32_t)i;
+                pv[j] = __builtin_amdgcn_raw_buffer_load_b128(src(s), off, 0, kAuxSc1);
+            }
+            if (s0 == 0)
+                acc = make_float4(bop(__uint_as_float(yu.x)), bop(__uint_as_float(yu.y)),
+                                  bop(__uint_as_float(yu.z)), bop(__uint_as_float(yu.w)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t s = s0 + j;
+                if (s >= n_slabs) break;
+                const float4 v = s == me ? own
+                                         : make_float4(__uint_as_float(pv[j].x), __uint_as_float(pv[j].y),
+                                                       __uint_as_float(pv[j].z), __uint_as_float(pv[j].w));
+                acc.x = __fadd_rn(acc.x, v.x);
+                acc.y = __fadd_rn(acc.y, v.y);
+                acc.z = __fadd_rn(acc.z, v.z);
+                acc.w = __fadd_rn(acc.w, v.w);
+            }
+        }
+        *reinterpret_cast<float4 *>(y + r0 + i) = acc;
+    }
+    for (int32_t i = hv + tid; i < hi; i += THREADS) {
+        float a = bop(y[r0 + i]);
+        for (int32_t s = 0; s < n_slabs; ++s) {
+            const float v = s == me ? yacc[i]
+                                    : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(src(s), 4u * i, 0, kAuxSc1));
+            a = __fadd_rn(a, v);
+        }
+        y[r0 + i] = a;
+    }
+}
+
 template <int THREADS>
 __device__ void slab_handoff(const float *yacc, int32_t *ctl, int32_t *s_word, float *y,
                              float *partials, int32_t n_rows, int32_t r0, int32_t nr,
@@ -227,19 +283,31 @@ __device__ __forceinline__ uint64_t handoff_snapshot(const int32_t *ctl, int32_t
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(ctl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int THREADS>
-__device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_word, float *y,
+template <int THREADS, bool BL>
+__device__ __forceinline__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_word, float *y,
                                    float *partials, int32_t n_rows, int32_t r0, int32_t nr,
                                    int32_t slab, int32_t n_slabs, bool y_vec, uint64_t old_started,
-                                   uint64_t snapshot) {
+                                   uint64_t snapshot, float beta, unsigned long long *ts) {
     const int32_t tid = threadIdx.x;
     const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
-    float *outp = slab == 0 ? y + r0 : partials + (int64_t)(slab - 1) * ps;
-    outp = slab == 0 ? outp : outp + r0;
-    const bool vec_out = slab != 0 || y_vec;
+    // BL: every slab publishes into partials[slab]; otherwise slab 0 into y, s >= 1 into partials[s-1].
+    float *outp = (BL || slab != 0) ? partials + (int64_t)(BL ? slab : slab - 1) * ps + r0 : y + r0;
+    const bool vec_out = BL || slab != 0 || y_vec;
     const int32_t part = ((nr + n_slabs - 1) / n_slabs + 3) & ~3;
     auto part_lo = [&](int32_t s) { return min(s * part, nr); };
     auto part_hi = [&](int32_t s) { return min((s + 1) * part, nr); };
+    auto combine = [&](int32_t q) {
+        if constexpr (BL)
+            combine_rows_bl<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec, beta, part_lo(q),
+                                     part_hi(q));
+        else
+            combine_rows<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec, part_lo(q), part_hi(q));
+    };
+    // Development timeline (ts != nullptr, thread 0): [0] published and drained, [1] arrival
+    // add returned, [2] every sibling seen, [3] combine stores drained.
+    auto stamp = [&](int k) {
+        if (ts != nullptr && tid == 0) ts[k] = wall_clock64();
+    };
     const uint64_t S = (uint64_t)n_slabs;
     if (tid == 0) {   // thread 0 holds the generation (handoff_begin)
         const uint64_t g = old_started / S;
@@ -258,9 +326,11 @@ __device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_w
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(0);
     if (tid == 0) {
         const int32_t add = 1 + (committed ? (1 << (8 + slab)) : 0);
         s_word[1] = __hip_atomic_fetch_add(arrive, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+        stamp(1);
         if (committed) {   // every sibling is resident: wait for all of them to publish
             int32_t a = s_word[1];
             while ((a & 0xFF) < n_slabs) {
@@ -269,22 +339,148 @@ __device__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_w
             }
             s_word[2] = a;
         }
+        stamp(2);
     }
     __syncthreads();
     const int32_t arrived = s_word[1];
-    if (committed)
-        combine_rows<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec, part_lo(slab),
-                              part_hi(slab));
+    if (committed) combine(slab);
     if ((arrived & 0xFF) == n_slabs) {
         // Last arriver: the parts of tiles that did not commit.
         const int32_t mask = (committed ? s_word[2] : arrived) >> 8;
         for (int32_t q = 0; q < n_slabs; ++q)
-            if (!((mask >> q) & 1))
-                combine_rows<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec,
-                                      part_lo(q), part_hi(q));
+            if (!((mask >> q) & 1)) combine(q);
     }
     if (tid == 0 && slab == 0)   // the next launch's word (see above)
         __hip_atomic_store(ctl + 2 + (g ^ 1u), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ts != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(3);
+    }
+}
+
+// Every row of the block, beta-last form (combine_rows_bl), S <= 4 and a 16-byte aligned y:
+// the loads of K row quads per thread (y and the other slabs' sums) go out before any add, so
+// the combiner pays about one memory latency per K * 4 * THREADS rows.
+template <int THREADS>
+__device__ __forceinline__ void combine_all_bl(const float *yacc, float *y, const float *partials, int64_t ps,
+                                               int32_t r0, int32_t nr, int32_t me, int32_t n_slabs, bool y_vec,
+                                               float beta) {
+    constexpr int K = 4;
+    if (n_slabs > 4 || !y_vec) {
+        combine_rows_bl<THREADS>(yacc, y, partials, ps, r0, nr, me, n_slabs, y_vec, beta, 0, nr);
+        return;
+    }
+    const int32_t tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
+    // The other slabs' sums, j-th other slab s = j + (j >= me); past S: an empty range (no request).
+    auto other = [&](int32_t j) {
+        const int32_t s = j + (j >= me ? 1 : 0);
+        return rsrc(partials + (int64_t)s * ps + r0, s < n_slabs ? (uint64_t)nr * 4 : 0);
+    };
+    const __amdgpu_buffer_rsrc_t o_src0 = other(0), o_src1 = other(1), o_src2 = other(2);
+    auto bop = [&](float v) { return beta != 1.0f ? __fmul_rn(v, beta) : v; };
+    const int32_t hv = nr & ~3;
+    for (int32_t i0 = 4 * tid; i0 < hv; i0 += 4 * THREADS * K) {
+        // pv[k][j]: the j-th other slab (s = j + (j >= me)); slots past S - 1: no request
+        u32x4 yu[K], pv[K][3];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t i = i0 + 4 * THREADS * k;
+            const uint32_t off = i < hv ? 4u * (uint32_t)i : 0xFFFFFFF0u;
+            yu[k] = __builtin_amdgcn_raw_buffer_load_b128(y_src, off, 0, 0);
+            pv[k][0] = __builtin_amdgcn_raw_buffer_load_b128(o_src0, off, 0, kAuxSc1);
+            pv[k][1] = __builtin_amdgcn_raw_buffer_load_b128(o_src1, off, 0, kAuxSc1);
+            pv[k][2] = __builtin_amdgcn_raw_buffer_load_b128(o_src2, off, 0, kAuxSc1);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t i = i0 + 4 * THREADS * k;
+            if (i >= hv) break;
+            const float4 own = *reinterpret_cast<const float4 *>(&yacc[i]);
+            float4 acc = make_float4(bop(__uint_as_float(yu[k].x)), bop(__uint_as_float(yu[k].y)),
+                                     bop(__uint_as_float(yu[k].z)), bop(__uint_as_float(yu[k].w)));
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (s >= n_slabs) break;
+                const u32x4 u = s < me ? pv[k][s < 3 ? s : 2] : pv[k][s > 0 ? s - 1 : 0];
+                const float4 v = s == me ? own
+                                         : make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
+                                                       __uint_as_float(u.z), __uint_as_float(u.w));
+                acc.x = __fadd_rn(acc.x, v.x);
+                acc.y = __fadd_rn(acc.y, v.y);
+                acc.z = __fadd_rn(acc.z, v.z);
+                acc.w = __fadd_rn(acc.w, v.w);
+            }
+            *reinterpret_cast<float4 *>(y + r0 + i) = acc;
+        }
+    }
+    if (hv < nr) combine_rows_bl<THREADS>(yacc, y, partials, ps, r0, nr, me, n_slabs, y_vec, beta, hv, nr);
+}
+
+// Combiner-tile hand-off (xband.h b2_combiner; beta-last sums).  The S - 1 other slab tiles
+// publish all their rows write-through into partials[slab], drain, pass a workgroup barrier
+// and add 1 to the generation's arrival word (MI355X_MICROARCH.md "Valid forms", row 1), then
+// leave.  The combiner -- when every sibling had started (the epoch snapshot), so they are all
+// resident and finish without waiting on anything -- polls that word until S - 1 have arrived
+// and combines every row: beta*y (plain loads: nobody else touches y in this form), the other
+// sums by sc1 loads, its own from LDS.  When a sibling had not started, the combiner publishes
+// too and the tile whose add brings the word to S combines (the last-arriver form), so no tile
+// ever waits on one that may not be resident.  Control words as slab_handoff_epoch's.
+template <int THREADS>
+__device__ __forceinline__ void slab_handoff_comb(const float *yacc, int32_t *ctl, int32_t *s_word, float *y, float *partials,
+                                  int32_t n_rows, int32_t r0, int32_t nr, int32_t slab, int32_t n_slabs,
+                                  int32_t comb, bool y_vec, uint64_t old_started, uint64_t snapshot, float beta,
+                                  unsigned long long *ts) {
+    const int32_t tid = threadIdx.x;
+    const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
+    auto stamp = [&](int k) {
+        if (ts != nullptr && tid == 0) ts[k] = wall_clock64();
+    };
+    const uint64_t S = (uint64_t)n_slabs;
+    if (tid == 0) {
+        const uint64_t g = old_started / S;
+        s_word[0] = snapshot - g * S >= S;   // every sibling had started
+        s_word[3] = (int32_t)(g & 1u);
+    }
+    __syncthreads();
+    const bool waits = slab == comb && s_word[0] != 0;
+    const uint32_t g = (uint32_t)s_word[3];
+    int32_t *arrive = ctl + 2 + g;
+    bool combines = waits;
+    if (!waits) {
+        publish_rows<THREADS>(yacc, partials + (int64_t)slab * ps + r0, true, 0, nr, nr);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(0);
+        if (tid == 0) {
+            s_word[1] = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+            stamp(1);
+            stamp(2);
+        }
+        __syncthreads();
+        combines = s_word[1] == n_slabs;   // the last of S publishers (a sibling had not started)
+    } else {
+        stamp(0);
+        if (tid == 0) {
+            int32_t a = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stamp(1);
+            while (a < n_slabs - 1) {
+                __builtin_amdgcn_s_sleep(2);
+                a = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            stamp(2);
+        }
+        __syncthreads();
+    }
+    if (combines) combine_all_bl<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec, beta);
+    if (tid == 0 && slab == 0)   // the next launch's word (slab_handoff_epoch)
+        __hip_atomic_store(ctl + 2 + (g ^ 1u), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ts != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        stamp(3);
+    }
 }
 
 }  // namespace

@@ -89,33 +89,60 @@ def with_env(key: str, value: str, fn):
             os.environ[key] = old
 
 
-def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int, slab0_cols: int | None = None):
+def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int, slab0_cols: int | None = None,
+                    beta_last: bool = False, term_slab=None, n_slabs: int | None = None):
     """The multi-slab band layouts' sum, restated on the oracle: each column slab summed in
     the reference's order (oracle.csr_spmv) -- slab 0 from beta*y, later slabs from -0.0 --
-    then the slab sums added in slab order in fp32.  Slab 0 covers [0, slab0_cols), slab
-    s >= 1 [slab0_cols + (s-1) slab_cols, slab0_cols + s slab_cols) (sm_info.xband_slab0_cols
-    / xband_slab_cols; even slabs when slab0_cols is None).  Bit-exact target for has_xband
-    2/3/4/5/6 with several slabs."""
+    then the slab sums added in slab order in fp32.  beta_last (sm_info.xband_beta_last, the
+    band2 / cband hand-off): every slab from -0.0, y = (((beta*y + P_0) + P_1) + ...), beta*y
+    as kernel.cc:10-29 forms it (y *= beta unless beta == 1).  Slab 0 covers [0, slab0_cols),
+    slab s >= 1 [slab0_cols + (s-1) slab_cols, slab0_cols + s slab_cols)
+    (sm_info.xband_slab0_cols / xband_slab_cols; even slabs when slab0_cols is None), unless
+    term_slab gives every term's slab (combiner-tile slabs differ per row block; slab_order_for).
+    Bit-exact target for has_xband 2/3/4/5/6 with several slabs."""
     import oracle
     rp = np.asarray(rp, np.int64)
     ci = np.asarray(ci)
     va = np.asarray(va, np.float32)
+    y0 = np.asarray(y0, np.float32)
     n = rp.size - 1
     n_cols = x.size
-    s0 = slab_cols if slab0_cols is None else slab0_cols
-    n_slabs = 1 + max(0, -(-(n_cols - s0) // slab_cols))
-    out = None
+    if term_slab is None:
+        s0 = slab_cols if slab0_cols is None else slab0_cols
+        n_slabs = 1 + max(0, -(-(n_cols - s0) // slab_cols))
+        term_slab = np.where(ci < s0, 0, 1 + (ci.astype(np.int64) - s0) // slab_cols)
+    bl = beta_last and n_slabs > 1
+    out = (y0 * np.float32(beta) if beta != 1.0 else y0.copy()) if bl else None
     for s in range(n_slabs):
-        lo = 0 if s == 0 else s0 + (s - 1) * slab_cols
-        hi = s0 + s * slab_cols
-        mask = (ci >= lo) & (ci < hi)
+        mask = term_slab == s
         cm = np.concatenate([[0], np.cumsum(mask)])
         rps = np.zeros(n + 1, np.int64)
         rps[1:] = cm[rp[1:]] - cm[rp[:-1]]
         rps = np.cumsum(rps)
-        if s == 0:
+        if s == 0 and not bl:
             p = oracle.csr_spmv(rps, ci[mask], va[mask], x, y0, alpha, beta)
         else:
             p = oracle.csr_spmv(rps, ci[mask], va[mask], x, np.full(n, -0.0, np.float32), alpha, 1.0)
         out = p if out is None else (out + p).astype(np.float32)
     return out
+
+
+def slab_order_for(info, rp, ci, va, x, y0, alpha, beta):
+    """slab_order_spmv with the slab geometry and hand-off form the matrix reports; combiner-tile
+    slabs (sm_info.xband_comb_cols > 0): in row block b the slab c = (b >> 1) % S is comb_cols
+    wide, the others xband_slab_cols (include/sparsematrix.h)."""
+    if not info["xband_comb_cols"]:
+        return slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"],
+                               beta_last=bool(info["xband_beta_last"]))
+    rp = np.asarray(rp, np.int64)
+    ci64 = np.asarray(ci).astype(np.int64)
+    S, sc, cc, br = info["xband_slabs"], info["xband_slab_cols"], info["xband_comb_cols"], info["xband_block_rows"]
+    row = np.repeat(np.arange(rp.size - 1, dtype=np.int64), np.diff(rp))
+    c = (row // br >> 1) % S
+    # slab s starts at s * sc + (s > c) * (cc - sc): find the largest s with start <= column
+    term_slab = np.zeros(ci64.size, np.int64)
+    for s in range(1, S):
+        lo = s * sc + np.where(s > c, cc - sc, 0)
+        term_slab[ci64 >= lo] = s
+    return slab_order_spmv(rp, ci, va, x, y0, alpha, beta, sc, None, beta_last=True, term_slab=term_slab,
+                           n_slabs=S)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle
-from gpu_util import (assert_terms_close, bits, slab_order_spmv, to_dev, to_host, torch_dev,
+from gpu_util import (assert_terms_close, bits, slab_order_for, to_dev, to_host, torch_dev,
                       uniform_csr)
 
 pytestmark = pytest.mark.gpu
@@ -51,7 +51,7 @@ def _check(M, info, rp, ci, va, x, y0, alpha, beta, algo="xband"):
     if info["xband_slabs"] == 1:
         want = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     else:
-        want = slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"])
+        want = slab_order_for(info, rp, ci, va, x, y0, alpha, beta)
     assert np.array_equal(bits(got), bits(want)), (alpha, beta, info["xband_slabs"])
     ref = oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta)
     _, absum = oracle.csr_spmv_f64(rp, ci, va, x, y0, alpha, beta)
@@ -150,7 +150,7 @@ def test_band2_special_values_and_signed_zeros(sm, kind, tall):
             M.spmv(to_dev(x), y, alpha, beta, algo="xband")
             got = to_host(y)
             want = (oracle.csr_spmv(rp, ci, va, x, y0, alpha, beta) if info["xband_slabs"] == 1
-                    else slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"]))
+                    else slab_order_for(info, rp, ci, va, x, y0, alpha, beta))
             assert np.array_equal(bits(got), bits(want))
 
 
@@ -174,7 +174,7 @@ def test_band2_repeated_launches_reset_handoff(sm, kind, tall):
     first = bits(to_host(ys[0]))
     for y in ys[1:]:
         assert np.array_equal(bits(to_host(y)), first)
-    want = slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
+    want = slab_order_for(info, rp, ci, va, to_host(x), y0, 1.0, 0.5)
     assert np.array_equal(first, bits(want))
 
 
@@ -218,7 +218,7 @@ def test_handoff_counter_across_32bit_boundary(sm, kind, slabs):
     rng = np.random.default_rng(32)
     x = to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32))
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
-    want = bits(slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"]))
+    want = bits(slab_order_for(info, rp, ci, va, to_host(x), y0, 1.0, 0.5))
     ys = [to_dev(y0) for _ in range(4)]
     for y in ys:
         M.spmv(x, y, 1.0, 0.5)
@@ -262,7 +262,7 @@ def test_cband_dma3_special_values_and_repeats(sm):
     x[-1] = np.inf                     # the last column, inside the last window
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
     y0[:300] = -0.0
-    want = slab_order_spmv(rp, ci, va, x, y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
+    want = slab_order_for(info, rp, ci, va, x, y0, 1.0, 0.5)
     xd = to_dev(x)
     ys = [to_dev(y0) for _ in range(6)]
     for y in ys:
@@ -288,15 +288,16 @@ def test_cband_dma3_config2_vs_slab_oracle(sm, tall):
     y0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
     y = y0.clone()
     M.spmv(x, y, 1.0, 0.5)
-    want = slab_order_spmv(rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
-                           1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
+    want = slab_order_for(info, rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy(), to_host(x), to_host(y0),
+                          1.0, 0.5)
     assert np.array_equal(bits(to_host(y)), bits(want))
 
 
 def test_band2_config2_equals_blocked(sm):
     """BASELINE config 2 (2^20 x 2^20, 16 terms/row): cband, band2 and the blocked kind
     built on the same 4 even slabs of 262144 columns sum each in the reference's order, so
-    their results are bit-identical."""
+    cband and band2 are bit-identical; the blocked kind too unless band2 / cband add beta*y
+    in the combine (sm_info.xband_beta_last), then both are within the bound."""
     torch = torch_dev()
     import sparsematrix_amd.synth as synth
     n = 1 << 20
@@ -317,8 +318,19 @@ def test_band2_config2_equals_blocked(sm):
     Mb2.spmv(x, y2, 1.3, 0.5)
     Mbl.spmv(x, yb, 1.3, 0.5)
     torch.cuda.synchronize()
-    assert torch.equal(y2.view(torch.int32), yb.view(torch.int32))
-    assert torch.equal(yc.view(torch.int32), yb.view(torch.int32))
+    assert torch.equal(yc.view(torch.int32), y2.view(torch.int32))
+    if not ic["xband_beta_last"]:
+        assert torch.equal(yc.view(torch.int32), yb.view(torch.int32))
+    else:
+        # The blocked kind starts slab 0 from beta*y, band2 / cband add beta*y first in the
+        # combine: the same four slab sums in another order, both within the bound.
+        assert i2["xband_beta_last"] and not ib["xband_beta_last"]
+        rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+        xh, y0h = to_host(x), to_host(y0)
+        ref = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.3, 0.5, threads=16)
+        _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.3, 0.5)
+        assert_terms_close(to_host(yc), ref, absum)
+        assert_terms_close(to_host(yb), ref, absum)
 
 
 def test_cband_falls_back_without_codebook(sm):
@@ -350,7 +362,7 @@ def test_config2_auto_full_size_vs_oracle(sm):
     got = to_host(y)
     rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
     xh, y0h = to_host(x), to_host(y0)
-    want = slab_order_spmv(rph, cih, vah, xh, y0h, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
+    want = slab_order_for(info, rph, cih, vah, xh, y0h, 1.0, 0.5)
     assert np.array_equal(bits(got), bits(want))
     ref = oracle.csr_spmv_mt(rph, cih, vah, xh, y0h, 1.0, 0.5, threads=16)
     _, absum = oracle.csr_spmv_f64(rph, cih, vah, xh, y0h, 1.0, 0.5)
@@ -404,7 +416,7 @@ def test_concurrent_spmvs_on_two_streams(sm):
     rng = np.random.default_rng(32)
     xs = [to_dev(rng.uniform(-1, 1, n_cols).astype(np.float32)) for _ in range(8)]
     y0 = rng.uniform(-1, 1, n_rows).astype(np.float32)
-    want = [slab_order_spmv(rp, ci, va, to_host(x), y0, 1.0, 0.5, info["xband_slab_cols"], info["xband_slab0_cols"])
+    want = [slab_order_for(info, rp, ci, va, to_host(x), y0, 1.0, 0.5)
             for x in xs]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     ys = [to_dev(y0) for _ in xs]
