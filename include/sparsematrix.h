@@ -155,10 +155,6 @@ typedef struct sm_info {
     int32_t xband_beta_last;    /* 1: the slab sums are added after beta*y -- y = (((beta*y +
                                    P_0) + P_1) + ...), every P_s summed from -0.0 (band2 / cband
                                    with several slabs); 0: slab 0 starts from beta*y          */
-    int32_t xband_comb_cols;    /* > 0: combiner-tile slabs -- in row block b the combiner slab
-                                   c = (b >> 1) % xband_slabs is xband_comb_cols wide, the others
-                                   xband_slab_cols: slab s = [s * slab_cols + (s > c ? comb_cols -
-                                   slab_cols : 0), ...) clipped to the columns               */
 } sm_info;
 
 /* ---- library ----------------------------------------------------------- */

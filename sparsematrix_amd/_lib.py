@@ -78,7 +78,6 @@ class SmInfo(C.Structure):
         ("hot_cols", C.c_int32), ("sweep_blocks", C.c_int32),
         ("exact_sell_slices", C.c_int64), ("exact_algo", C.c_int32), ("xband_slab0_cols", C.c_int32),
         ("merge_stage", C.c_int32), ("xband_beta_last", C.c_int32),
-        ("xband_comb_cols", C.c_int32),
     ]
 
 

@@ -31,7 +31,10 @@ struct TileOut {
     bool ok = true;
 };
 
-using Seg = B2Seg;
+// A row's run of terms inside one chunk: row in block, first term index, count.
+struct Seg {
+    int32_t rl, s, n;
+};
 
 // Lanes inside a chunk: segments of 2+ terms take consecutive lanes first (the
 // kernel passes a running sum up the lanes), then the single terms go to the two
@@ -418,19 +421,9 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
 
 }  // namespace
 
-void b2_emit_chunk(uint32_t *band_ent, int c, const std::vector<B2Seg> &segs, const int32_t *col,
-                   const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom) {
-    emit_chunk(band_ent, c, segs, col, val, ids, clo_al, geom);
-}
-
-void b2_balance_chunks(std::vector<std::vector<B2Seg>> &cs, int nc, const int32_t *col, int32_t clo_al,
-                       int32_t span) {
-    balance_chunks(cs, nc, col, clo_al, span);
-}
-
 bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids, B2Geom geom,
-                 int32_t slab0_permille, int32_t comb_permille) {
+                 int32_t slab0_permille) {
     out = Band2Host();
     out.codebook = ids != nullptr;
     out.geom = geom;
@@ -460,22 +453,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
             s0 = sc;
         }
     }
-    // Combiner tiles (xband.h b2_combiner): the combiner's slab comb_permille / 1000 of the even
-    // share, the others split the rest; slab 0's width option does not apply then.
-    const bool comb = ns > 1 && comb_permille >= 1000;
-    int64_t cc = sc;
-    if (comb) {
-        cc = std::min<int64_t>(n_cols, (sc * comb_permille / 1000 + 255) & ~(int64_t)255);
-        sc = std::max<int64_t>(256, ((n_cols - cc + ns - 2) / (ns - 1) + 255) & ~(int64_t)255);
-        s0 = sc;
-    }
-    auto slab_lo_b = [&](int64_t b, int64_t s) -> int64_t {
-        if (comb) {
-            const int64_t c = b2_combiner(b, (int32_t)ns);
-            return std::min<int64_t>(n_cols, s * sc + (s > c ? cc - sc : 0));
-        }
-        return s == 0 ? (int64_t)0 : std::min<int64_t>(n_cols, s0 + (s - 1) * sc);
-    };
+    auto slab_lo = [&](int64_t s) { return s == 0 ? (int64_t)0 : std::min<int64_t>(n_cols, s0 + (s - 1) * sc); };
     const int64_t ntile = nblk * ns;
     if (ntile >= ((int64_t)1 << 30)) return false;
     std::vector<TileOut> tiles((size_t)ntile);
@@ -485,8 +463,8 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
         th.emplace_back([&, t] {
             for (int64_t i = t; i < ntile; i += nthr) {
                 const int64_t b = i / ns, s = i % ns;
-                build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), slab_lo_b(b, s),
-                           slab_lo_b(b, s + 1), geom, tiles[(size_t)i]);
+                build_tile(rp, col, val, ids, b * br, std::min<int64_t>(n_rows, (b + 1) * br), slab_lo(s),
+                           slab_lo(s + 1), geom, tiles[(size_t)i]);
             }
         });
     for (auto &x : th) x.join();
@@ -495,8 +473,6 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out.n_slabs = (int32_t)ns;
     out.slab_cols = (int32_t)sc;
     out.slab0_cols = (int32_t)s0;
-    out.comb_permille = comb ? comb_permille : 0;
-    out.comb_cols = comb ? (int32_t)cc : 0;
     out.tile_band_start.resize((size_t)ntile + 1);
     int64_t nb = 0;
     for (int64_t i = 0; i < ntile; i++) {

@@ -204,7 +204,6 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     if (const char *e = dev_env("SM_BAND_TALL")) r.band_tall = atoi(e);
     if (const char *e = dev_env("SM_BAND2_SLABS")) r.band_slabs = atoi(e);
     if (const char *e = dev_env("SM_BAND_SLAB0")) r.band_slab0_permille = atoi(e);
-    if (const char *e = dev_env("SM_B2_COMB")) r.band_comb_permille = atoi(e);
     if (const char *e = dev_env("SM_XBAND_GBAND")) r.gather_band_log2 = atoi(e);
     if (const char *e = dev_env("SM_RELABEL")) r.relabel = atoi(e);
     if (const char *e = dev_env("SM_SELL")) r.sell = atoi(e) ? -1 : 0;
@@ -342,8 +341,7 @@ bool want_xband(const sm_matrix *m) {
 // bands that would be < 70 % full fall back to wide.
 static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t n_cols, int64_t nnz,
                              const int32_t *rp, const int32_t *col, const float *val, XbKind kind,
-                             int32_t geo_opt, int32_t slabs, bool forced, int32_t slab0_permille = 1000,
-                             int32_t comb_permille = 0) {
+                             int32_t geo_opt, int32_t slabs, bool forced, int32_t slab0_permille = 1000) {
     const bool dma3 = geo_opt != 6;
     const B2Geom geom = dma3 ? (kind == kXbCband ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
     const int64_t br = std::min<int64_t>(geom.block_rows, n_rows);
@@ -360,8 +358,7 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     // them mostly dummies (wide or very sparse matrices), the padding would cost more HBM
     // bytes than the layout saves -- decline unless forced (SM_LAYOUT_BAND2 / CBAND).
     auto fits = [&](const B2Geom &gg) {
-        if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, gg, slab0_permille,
-                         comb_permille))
+        if (!band2_build(rp, col, val, n_rows, n_cols, want, bh, cb ? ids.data() : nullptr, gg, slab0_permille))
             return false;
         return forced || bh.n_bands == 0 ||
                (double)bh.real_terms >= 0.7 * (double)bh.n_bands * gg.chunks() * 64;
@@ -409,8 +406,6 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
     d.n_slabs = bh.n_slabs;
     d.slab_bands = bh.slab_cols;
     d.slab0_cols = bh.slab0_cols;
-    d.comb = bh.comb_permille > 0 ? 1 : 0;
-    d.comb_cols = bh.comb_cols;
     d.n_chunks = bh.n_bands * g.chunks();
     d.max_chunks_per_band = bh.max_bands_per_tile;
     d.n_blocks = bh.n_blocks;
@@ -426,7 +421,7 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
     // shorten the kernel (kB2Slab0Permille), so AUTO keeps even slabs; the option stays.
     const int32_t p0 = m->opts.band_slab0_permille > 0 ? m->opts.band_slab0_permille : kB2Slab0Permille;
     return build_band2(m, m->plan.xb, m->n_rows, m->n_cols, m->nnz, rp, col, val, kind,
-                       m->opts.band_tall, m->opts.band_slabs, kind_forced(m), p0, m->opts.band_comb_permille);
+                       m->opts.band_tall, m->opts.band_slabs, kind_forced(m), p0);
 }
 
 // Gathered chunk bands (gcb.h, kernels_gcb.hip): 32K-row tiles where the rows make at
@@ -1463,7 +1458,8 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
     // The band / sell builders run on the host (band2.cpp, xband.cpp, sell.cpp): the
     // columns come down for any of them, the values only for the layout that stores
     // them (4 + 4 bytes per term over PCIe once, at creation).
-    if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell || want_sweep(m.get()))) {
+    if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell || want_sweep(m.get()) ||
+                        want_merge_stage(m.get()))) {
         std::vector<int32_t> ch((size_t)nnz);
         std::vector<float> vh;
         auto values = [&]() -> sm_status {
@@ -1543,9 +1539,8 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
         : (int32_t)std::min<int64_t>((int64_t)m->plan.xb.slab_bands * m->plan.xb.band_cols, INT32_MAX);
     info->xband_slab0_cols = m->plan.xb.slab0_cols > 0 ? m->plan.xb.slab0_cols : info->xband_slab_cols;
     info->merge_stage = m->plan.d_mstage_w ? 1 : 0;
-    info->xband_beta_last = (SM_B2_BL || m->plan.xb.comb) && m->plan.xb.n_blocks > 0 && m->plan.xb.n_slabs > 1 &&
+    info->xband_beta_last = SM_B2_BL && m->plan.xb.n_blocks > 0 && m->plan.xb.n_slabs > 1 &&
                             (m->plan.xb.kind == kXbBand2 || m->plan.xb.kind == kXbCband);
-    info->xband_comb_cols = m->plan.xb.n_blocks > 0 && m->plan.xb.comb ? m->plan.xb.comb_cols : 0;
     info->device_bytes = m->device_bytes;
     info->col_relabel = m->plan.n_relabel > 0 ? 1 : 0;
     info->sell_slices = m->plan.sell.n_slices;

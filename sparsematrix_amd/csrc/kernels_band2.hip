@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
-    int32_t *__restrict__ ctl, float alpha, float beta, int32_t comb) {
+    int32_t *__restrict__ ctl, float alpha, float beta) {
     static_assert(GEO == 0 || GEO == 4, "wide or dma3");
     constexpr bool kLd = GEO == 4;   // dma3: wave kLdWave stages x, the others apply
     constexpr B2Geom G = kLd ? (CB ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // zero y), all loads in flight.
     constexpr int kQ = BROWS / (4 * kB2Threads);
     const bool y_vec = ((uintptr_t)(y + r0) & 15) == 0;
-    const bool y_first = slab == 0 && (n_slabs == 1 || (!SM_B2_BL && !comb));
+    const bool y_first = slab == 0 && (n_slabs == 1 || !SM_B2_BL);
     float4 yv[kQ];
     if (y_first) {
         const __amdgpu_buffer_rsrc_t yi_src = rsrc(y + r0, (uint64_t)nr * 4);
@@ -547,13 +547,9 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
         if (blockIdx.x < 4096) ts = &g_b2_ts[kTs * blockIdx.x + 3];
     }
 #endif
-    if (comb)
-        slab_handoff_comb<kB2Threads>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials, n_rows, r0, nr,
-                                      slab, n_slabs, b2_combiner(b, n_slabs), y_vec, old_started, snap, beta, ts);
-    else
-        slab_handoff_epoch<kB2Threads, SM_B2_BL != 0>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials,
-                                                      n_rows, r0, nr, slab, n_slabs, y_vec, old_started, snap,
-                                                      beta, ts);
+    slab_handoff_epoch<kB2Threads, SM_B2_BL != 0>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials,
+                                                  n_rows, r0, nr, slab, n_slabs, y_vec, old_started, snap, beta,
+                                                  ts);
     flush_prof();
 }
 
@@ -565,7 +561,7 @@ hipError_t launch_prof(int prof, dim3 grid, hipStream_t s, const XbandDev &xb, i
 #define SM_B2P(P)                                                                                   \
     hipLaunchKernelGGL((spmv_band2_kernel<true, GEO, P>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols, \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.comb)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
     if (prof == 1) {
         if (GEO != 4) return hipErrorInvalidValue;
         unsigned long long h[8] = {};
@@ -664,7 +660,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
 #define SM_B2(C, T)                                                                                 \
     hipLaunchKernelGGL((spmv_band2_kernel<C, T, 0>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.comb)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
     if (dma3) {
         if (cb) SM_B2(true, 4); else SM_B2(false, 4);
     } else {

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     const int32_t tile_rows = r1 - r0, tile_nnz = z1 - z0;
     // Stage: the slice's terms (every load issued before the first is used) and row ends.
     if constexpr (STAGE) {
+        static_assert(kMgThreads == 256, "one scaled codebook entry per thread");
         s_tab[tid] = __fmul_rn(stab[tid], alpha);
         uint32_t w[kMgIpt];
         uint32_t zz[kMgIpt];

@@ -56,7 +56,6 @@ struct BuildOpts {
     int32_t exact_sell = 0;   // 0 auto, 1 always, -1 never (sm_build_opts.exact_sell)
     int32_t band_slab0_permille = 0;   // 0 auto (sm_build_opts.band_slab0_permille)
     int32_t merge_stage = 0;           // sm_build_opts.merge_stage
-    int32_t band_comb_permille = 0;    // combiner-tile hand-off (xband.h b2_combiner); 0 off
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
@@ -78,8 +77,6 @@ struct XbandDev {
     int32_t block_rows = 0, band_cols = 0, n_blocks = 0, n_bands = 0;
     int32_t n_slabs = 1, slab_bands = 0;   // tiles = n_blocks * n_slabs
     int32_t slab0_cols = 0;           // band2 / cband: columns of slab 0 (others: slab_bands)
-    int32_t comb = 0;                 // band2 / cband: 1 = combiner-tile hand-off (xband.h b2_combiner)
-    int32_t comb_cols = 0;            // the combiner's slab width (comb = 1)
     int64_t n_chunks = 0;
     int64_t max_chunks_per_band = 0;
     int32_t *d_chunk_start = nullptr;

@@ -11,8 +11,9 @@
 // B[4j + (l >> 4)][l & 15] (cdna_hip_programming.md, the f32 16x16x4 operand map): the 16
 // lanes of one term read its X row as 16 consecutive 8-byte pairs (one 128-byte line),
 // half 0 taking the even columns and half 1 the odd ones; D/C rows 4 (l >> 4) + r,
-// column l & 15 (the standard map).  No LDS: the B operand comes straight from the
-// gather into registers.
+// column l & 15 (the standard map).  Two forms: spmm_mfma_kernel takes the B operand
+// straight from the gather into registers; spmm_mfma_lds_kernel (the one SM_ALGO_MFMA runs)
+// stages the gathered X rows through LDS by LDS-DMA and reads the B operand back from there.
 //
 // Arithmetic: the f32 MFMA is an exact fma chain in k order (MI355X_MICROARCH.md: "exact
 // f32 (= fmaf chain, bitwise)"), so each output is beta*y followed by fma(fl(v*alpha), x,

@@ -13,12 +13,6 @@
 #define SM_B2_BL 1
 #endif
 
-#ifdef __HIPCC__
-#define SM_HD __host__ __device__
-#else
-#define SM_HD
-#endif
-
 namespace smamd {
 
 // Entry word: bits [0, C) column in band, [C, C+K) rank inside the row's segment
@@ -149,9 +143,6 @@ struct Band2Host {
     B2Geom geom = kB2Wide;
     int32_t block_rows = 0, n_blocks = 0, n_slabs = 0, slab_cols = 0;
     int32_t slab0_cols = 0;              // slab 0 = [0, slab0_cols), slab s >= 1 = [slab0 + (s-1) slab_cols, ...)
-    // Combiner tiles (comb_permille >= 1000): slab s of block b = [slab_lo(b, s), slab_lo(b, s + 1)),
-    // the combiner's slab comb_cols wide, the others slab_cols (the last one clipped).
-    int32_t comb_permille = 0, comb_cols = 0;
     int32_t max_bands_per_tile = 0;
     int64_t n_bands = 0;                 // over all tiles
     std::vector<int32_t> tile_band_start;   // n_blocks * n_slabs + 1 (tile t = b * S + s)
@@ -159,16 +150,6 @@ struct Band2Host {
     std::vector<uint32_t> ent;              // 4096 per band
     int64_t real_terms = 0;                 // for the padding report
 };
-
-// Combiner-tile hand-off (band2 / cband with several slabs, comb_permille >= 1000): in row block
-// b the slab tile b2_combiner(b, S) combines the whole block.  Its slab is comb_permille / 1000
-// of an even share wide and the other S - 1 slabs split the rest, so those end their band loops
-// first, publish all their sums (write-through) and leave; the combiner, ending last, adds
-// beta*y and the S slab sums in slab order for every row of the block itself -- after its loop
-// only the poll of the arrival word and the loads of the others' sums, no publish and no
-// second round trip.  (b >> 1) spreads the combiners over all 8 XCDs when S = 4 (blocks 2k and
-// 2k + 1 sit on opposite XCD halves under round-robin dispatch; speed only, never correctness).
-SM_HD inline int32_t b2_combiner(int64_t b, int32_t n_slabs) { return (int32_t)((b >> 1) % n_slabs); }
 
 // Returns false when the layout does not apply: unsorted columns or size limits
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).
@@ -179,18 +160,7 @@ SM_HD inline int32_t b2_combiner(int64_t b, int32_t n_slabs) { return (int32_t)(
 constexpr int32_t kB2Slab0Permille = 1000;
 bool band2_build(const int32_t *row_ptr, const int32_t *col, const float *val, int64_t n_rows,
                  int64_t n_cols, int32_t n_slabs, Band2Host &out, const uint8_t *ids = nullptr,
-                 B2Geom geom = kB2Wide, int32_t slab0_permille = 1000, int32_t comb_permille = 0);
-
-// A row's run of terms inside one chunk: row in block, first term index, count.
-struct B2Seg {
-    int32_t rl, s, n;
-};
-// The band builder's chunk emitter (bank-aware lane placement, band2.cpp) and its cross-chunk
-// bank balance, for other builders of codebook chunks (ro.cpp): chunk c of a band slot.
-void b2_emit_chunk(uint32_t *band_ent, int c, const std::vector<B2Seg> &segs, const int32_t *col,
-                   const float *val, const uint8_t *ids, int32_t clo_al, B2Geom geom);
-void b2_balance_chunks(std::vector<std::vector<B2Seg>> &cs, int nc, const int32_t *col, int32_t clo_al,
-                       int32_t span);
+                 B2Geom geom = kB2Wide, int32_t slab0_permille = 1000);
 
 // Codebook of a value array: table[ids[e]] has the bits of val[e] for every e; false
 // when there are more than 255 distinct bit patterns (table then undefined).

@@ -359,129 +359,5 @@ __device__ __forceinline__ void slab_handoff_epoch(const float *yacc, int32_t *c
     }
 }
 
-// Every row of the block, beta-last form (combine_rows_bl), S <= 4 and a 16-byte aligned y:
-// the loads of K row quads per thread (y and the other slabs' sums) go out before any add, so
-// the combiner pays about one memory latency per K * 4 * THREADS rows.
-template <int THREADS>
-__device__ __forceinline__ void combine_all_bl(const float *yacc, float *y, const float *partials, int64_t ps,
-                                               int32_t r0, int32_t nr, int32_t me, int32_t n_slabs, bool y_vec,
-                                               float beta) {
-    constexpr int K = 4;
-    if (n_slabs > 4 || !y_vec) {
-        combine_rows_bl<THREADS>(yacc, y, partials, ps, r0, nr, me, n_slabs, y_vec, beta, 0, nr);
-        return;
-    }
-    const int32_t tid = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t y_src = rsrc(y + r0, (uint64_t)nr * 4);
-    // The other slabs' sums, j-th other slab s = j + (j >= me); past S: an empty range (no request).
-    auto other = [&](int32_t j) {
-        const int32_t s = j + (j >= me ? 1 : 0);
-        return rsrc(partials + (int64_t)s * ps + r0, s < n_slabs ? (uint64_t)nr * 4 : 0);
-    };
-    const __amdgpu_buffer_rsrc_t o_src0 = other(0), o_src1 = other(1), o_src2 = other(2);
-    auto bop = [&](float v) { return beta != 1.0f ? __fmul_rn(v, beta) : v; };
-    const int32_t hv = nr & ~3;
-    for (int32_t i0 = 4 * tid; i0 < hv; i0 += 4 * THREADS * K) {
-        // pv[k][j]: the j-th other slab (s = j + (j >= me)); slots past S - 1: no request
-        u32x4 yu[K], pv[K][3];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int32_t i = i0 + 4 * THREADS * k;
-            const uint32_t off = i < hv ? 4u * (uint32_t)i : 0xFFFFFFF0u;
-            yu[k] = __builtin_amdgcn_raw_buffer_load_b128(y_src, off, 0, 0);
-            pv[k][0] = __builtin_amdgcn_raw_buffer_load_b128(o_src0, off, 0, kAuxSc1);
-            pv[k][1] = __builtin_amdgcn_raw_buffer_load_b128(o_src1, off, 0, kAuxSc1);
-            pv[k][2] = __builtin_amdgcn_raw_buffer_load_b128(o_src2, off, 0, kAuxSc1);
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int32_t i = i0 + 4 * THREADS * k;
-            if (i >= hv) break;
-            const float4 own = *reinterpret_cast<const float4 *>(&yacc[i]);
-            float4 acc = make_float4(bop(__uint_as_float(yu[k].x)), bop(__uint_as_float(yu[k].y)),
-                                     bop(__uint_as_float(yu[k].z)), bop(__uint_as_float(yu[k].w)));
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (s >= n_slabs) break;
-                const u32x4 u = s < me ? pv[k][s < 3 ? s : 2] : pv[k][s > 0 ? s - 1 : 0];
-                const float4 v = s == me ? own
-                                         : make_float4(__uint_as_float(u.x), __uint_as_float(u.y),
-                                                       __uint_as_float(u.z), __uint_as_float(u.w));
-                acc.x = __fadd_rn(acc.x, v.x);
-                acc.y = __fadd_rn(acc.y, v.y);
-                acc.z = __fadd_rn(acc.z, v.z);
-                acc.w = __fadd_rn(acc.w, v.w);
-            }
-            *reinterpret_cast<float4 *>(y + r0 + i) = acc;
-        }
-    }
-    if (hv < nr) combine_rows_bl<THREADS>(yacc, y, partials, ps, r0, nr, me, n_slabs, y_vec, beta, hv, nr);
-}
-
-// Combiner-tile hand-off (xband.h b2_combiner; beta-last sums).  The S - 1 other slab tiles
-// publish all their rows write-through into partials[slab], drain, pass a workgroup barrier
-// and add 1 to the generation's arrival word (MI355X_MICROARCH.md "Valid forms", row 1), then
-// leave.  The combiner -- when every sibling had started (the epoch snapshot), so they are all
-// resident and finish without waiting on anything -- polls that word until S - 1 have arrived
-// and combines every row: beta*y (plain loads: nobody else touches y in this form), the other
-// sums by sc1 loads, its own from LDS.  When a sibling had not started, the combiner publishes
-// too and the tile whose add brings the word to S combines (the last-arriver form), so no tile
-// ever waits on one that may not be resident.  Control words as slab_handoff_epoch's.
-template <int THREADS>
-__device__ __forceinline__ void slab_handoff_comb(const float *yacc, int32_t *ctl, int32_t *s_word, float *y, float *partials,
-                                  int32_t n_rows, int32_t r0, int32_t nr, int32_t slab, int32_t n_slabs,
-                                  int32_t comb, bool y_vec, uint64_t old_started, uint64_t snapshot, float beta,
-                                  unsigned long long *ts) {
-    const int32_t tid = threadIdx.x;
-    const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
-    auto stamp = [&](int k) {
-        if (ts != nullptr && tid == 0) ts[k] = wall_clock64();
-    };
-    const uint64_t S = (uint64_t)n_slabs;
-    if (tid == 0) {
-        const uint64_t g = old_started / S;
-        s_word[0] = snapshot - g * S >= S;   // every sibling had started
-        s_word[3] = (int32_t)(g & 1u);
-    }
-    __syncthreads();
-    const bool waits = slab == comb && s_word[0] != 0;
-    const uint32_t g = (uint32_t)s_word[3];
-    int32_t *arrive = ctl + 2 + g;
-    bool combines = waits;
-    if (!waits) {
-        publish_rows<THREADS>(yacc, partials + (int64_t)slab * ps + r0, true, 0, nr, nr);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        stamp(0);
-        if (tid == 0) {
-            s_word[1] = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-            stamp(1);
-            stamp(2);
-        }
-        __syncthreads();
-        combines = s_word[1] == n_slabs;   // the last of S publishers (a sibling had not started)
-    } else {
-        stamp(0);
-        if (tid == 0) {
-            int32_t a = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            stamp(1);
-            while (a < n_slabs - 1) {
-                __builtin_amdgcn_s_sleep(2);
-                a = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            stamp(2);
-        }
-        __syncthreads();
-    }
-    if (combines) combine_all_bl<THREADS>(yacc, y, partials, ps, r0, nr, slab, n_slabs, y_vec, beta);
-    if (tid == 0 && slab == 0)   // the next launch's word (slab_handoff_epoch)
-        __hip_atomic_store(ctl + 2 + (g ^ 1u), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ts != nullptr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        stamp(3);
-    }
-}
-
 }  // namespace
 }  // namespace smamd

@@ -98,8 +98,7 @@ def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int, slab0_cols: 
     as kernel.cc:10-29 forms it (y *= beta unless beta == 1).  Slab 0 covers [0, slab0_cols),
     slab s >= 1 [slab0_cols + (s-1) slab_cols, slab0_cols + s slab_cols)
     (sm_info.xband_slab0_cols / xband_slab_cols; even slabs when slab0_cols is None), unless
-    term_slab gives every term's slab (combiner-tile slabs differ per row block; slab_order_for).
-    Bit-exact target for has_xband 2/3/4/5/6 with several slabs."""
+    term_slab gives every term's slab.  Bit-exact target for has_xband 2/3/4/5/6 with several slabs."""
     import oracle
     rp = np.asarray(rp, np.int64)
     ci = np.asarray(ci)
@@ -128,21 +127,6 @@ def slab_order_spmv(rp, ci, va, x, y0, alpha, beta, slab_cols: int, slab0_cols: 
 
 
 def slab_order_for(info, rp, ci, va, x, y0, alpha, beta):
-    """slab_order_spmv with the slab geometry and hand-off form the matrix reports; combiner-tile
-    slabs (sm_info.xband_comb_cols > 0): in row block b the slab c = (b >> 1) % S is comb_cols
-    wide, the others xband_slab_cols (include/sparsematrix.h)."""
-    if not info["xband_comb_cols"]:
-        return slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"],
-                               beta_last=bool(info["xband_beta_last"]))
-    rp = np.asarray(rp, np.int64)
-    ci64 = np.asarray(ci).astype(np.int64)
-    S, sc, cc, br = info["xband_slabs"], info["xband_slab_cols"], info["xband_comb_cols"], info["xband_block_rows"]
-    row = np.repeat(np.arange(rp.size - 1, dtype=np.int64), np.diff(rp))
-    c = (row // br >> 1) % S
-    # slab s starts at s * sc + (s > c) * (cc - sc): find the largest s with start <= column
-    term_slab = np.zeros(ci64.size, np.int64)
-    for s in range(1, S):
-        lo = s * sc + np.where(s > c, cc - sc, 0)
-        term_slab[ci64 >= lo] = s
-    return slab_order_spmv(rp, ci, va, x, y0, alpha, beta, sc, None, beta_last=True, term_slab=term_slab,
-                           n_slabs=S)
+    """slab_order_spmv with the slab geometry and hand-off form the matrix reports."""
+    return slab_order_spmv(rp, ci, va, x, y0, alpha, beta, info["xband_slab_cols"], info["xband_slab0_cols"],
+                           beta_last=bool(info["xband_beta_last"]))

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Development check of the band2 / cband slab hand-off forms (SM_LIB_PATH = a -DSM_DEV build,
-SM_B2_COMB = the combiner slab's permille): config 2 and two smaller shapes, several launches
-and graph replays, every result bit for bit against the slab-order restatement
-(tests/gpu_util.slab_order_for) for the geometry the matrix reports."""
+"""Development check of a band2 / cband slab hand-off build (SM_LIB_PATH = a -DSM_DEV build):
+config 2 and two smaller shapes, several launches and graph replays, every result bit for bit
+against the slab-order restatement (tests/gpu_util.slab_order_for) for the geometry and hand-off
+form the matrix reports."""
 import os
 import sys
 
@@ -44,7 +44,7 @@ def main():
                 ok = np.array_equal(bits(y.cpu().numpy()), want)
                 if not ok:
                     print(name, "MISMATCH", alpha, beta, rep, {k: info[k] for k in (
-                        "has_xband", "xband_slabs", "xband_slab_cols", "xband_comb_cols", "xband_beta_last")})
+                        "has_xband", "xband_slabs", "xband_slab_cols", "xband_beta_last")})
                     sys.exit(3)
         # graph replays of 5 SpMVs on one y: compare with 5 eager ones
         y = y0.clone()
@@ -60,7 +60,7 @@ def main():
             graph.replay()
             torch.cuda.synchronize()
             assert torch.equal(y.view(torch.int32), ye.view(torch.int32)), name
-        print(name, "ok", {k: info[k] for k in ("has_xband", "xband_slabs", "xband_slab_cols", "xband_comb_cols",
+        print(name, "ok", {k: info[k] for k in ("has_xband", "xband_slabs", "xband_slab_cols",
                                                  "xband_beta_last")}, flush=True)
 
 

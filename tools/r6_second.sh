@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6, second GPU session: correctness of the beta-last and combiner-tile hand-offs
-# (tools/comb_check.py, bit for bit), then tile timelines and an alternating A/B of the bench's
+# (tools/handoff_check.py, bit for bit), then tile timelines and an alternating A/B of the bench's
 # config-2 line: a = round-5 hand-off (SM_B2_BL=0), b = beta-last, cNNNN = combiner tiles with
 # the combiner slab at NNNN permille (SM_B2_COMB).
 set -o pipefail
@@ -9,9 +9,9 @@ OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 B=$ROOT/build/dev_b/libsparsematrix_amd.so
-SM_LIB_PATH=$B timeout -k 10 300 python -u tools/comb_check.py > "$OUT/r6_check_b.txt" 2>&1 || { tail -20 "$OUT/r6_check_b.txt"; exit 21; }
+SM_LIB_PATH=$B timeout -k 10 300 python -u tools/handoff_check.py > "$OUT/r6_check_b.txt" 2>&1 || { tail -20 "$OUT/r6_check_b.txt"; exit 21; }
 cat "$OUT/r6_check_b.txt"
-SM_B2_COMB=1120 SM_LIB_PATH=$B timeout -k 10 300 python -u tools/comb_check.py > "$OUT/r6_check_c.txt" 2>&1 || { tail -20 "$OUT/r6_check_c.txt"; exit 22; }
+SM_B2_COMB=1120 SM_LIB_PATH=$B timeout -k 10 300 python -u tools/handoff_check.py > "$OUT/r6_check_c.txt" 2>&1 || { tail -20 "$OUT/r6_check_c.txt"; exit 22; }
 cat "$OUT/r6_check_c.txt"
 run_tl() {   # name lib [comb]
   SM_B2_COMB=${3:-0} SM_B2_TS_DUMP=1 SM_LIB_PATH=$2 SM_BAND2_PROF=2 timeout -k 10 150 python -u tools/cband_prof.py > "$OUT/r6_tl2_$1.txt" 2>&1 || { tail -20 "$OUT/r6_tl2_$1.txt"; exit 23; }
