@@ -15,10 +15,15 @@
 //      beta*y and is written at once, in the reference's order (kernel.cc:780-796) -- bit-exact;
 //   4. rows cut between threads: each thread leaves the open row's partial (a "tail") and the
 //      partial of a row it finished but did not start (a "head"); a segmented scan over the
-//      tails (fixed tree order) joins the cut rows inside the workgroup, y = (start part +
-//      middle parts) + end part -- within 1e-6 * sum|terms| of the reference, deterministic;
+//      tails joins the cut rows inside the workgroup -- per wavefront by __shfl_up
+//      (ds_bpermute; Hillis-Steele, six rounds, no barrier), then one cross-wave step that adds
+//      the earlier waves' ends to the lanes whose row began before their wave -- y = (start
+//      part + middle parts) + end part: within 1e-6 * sum|terms| of the reference,
+//      deterministic (a fixed tree);
 //   5. rows cut between workgroups leave one record per workgroup (its first row's end part,
-//      its last row's open part); spmv_merge_fixup_kernel adds them in workgroup order.
+//      its last row's open part); spmv_merge_fixup_kernel joins them from the row's start
+//      workgroup (found from the row pointer): in order by one thread, or -- rows over more
+//      than 64 workgroups -- by the whole wavefront in a fixed tree.
 #include "sm_internal.h"
 #include "xband_dev.h"
 
@@ -55,8 +60,11 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     __shared__ int32_t s_first;   // the workgroup's first row, when it began in an earlier one
     __shared__ float s_first_val;
     __shared__ float s_tab[STAGE ? 256 : 1];   // fl(table[id] * alpha)
-    __shared__ int32_t t_row[kMgThreads], t_flag[2][kMgThreads], t_sf[2][kMgThreads];
-    __shared__ float t_val[2][kMgThreads];
+    constexpr int kWaves = kMgThreads / 64;
+    __shared__ int32_t t_row[kMgThreads], t_sf[kMgThreads];
+    __shared__ float t_val[kMgThreads];
+    __shared__ float w_val[kWaves];   // each wave's last lane after the wave scan
+    __shared__ int32_t w_fs[kWaves];
     const int tid = threadIdx.x;
     const int2 c0 = corner[blockIdx.x], c1 = corner[blockIdx.x + 1];
     const int32_t r0 = c0.x, z0 = c0.y, r1 = c1.x, z1 = c1.y;
@@ -145,31 +153,39 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     }
     // Tails: a segmented inclusive scan over threads (segments = runs of one cut row; a run
     // starts at a thread that saw the row's start or follows a thread without that row).
+    // fs bit 0: the segment's start is at or before this lane; bit 1: that start was fresh.
     t_row[tid] = open ? r0 + ri : -1;
     __syncthreads();
-    {
-        const bool start = !open || tid == 0 || t_row[tid - 1] != t_row[tid] || fresh;
-        t_val[0][tid] = open ? acc : 0.0f;
-        t_flag[0][tid] = start;
-        t_sf[0][tid] = open && fresh;
+    const bool seg_start = !open || tid == 0 || t_row[tid - 1] != t_row[tid] || fresh;
+    float tv = open ? acc : 0.0f;
+    int32_t fs = (seg_start ? 1 : 0) | (open && fresh ? 2 : 0);
+    const int32_t lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {   // every lane shifts before any updates: lockstep wave
+        const float pv = __shfl_up(tv, d, 64);
+        const int32_t pfs = __shfl_up(fs, d, 64);
+        if (lane >= d && !(fs & 1)) {
+            tv = __fadd_rn(pv, tv);
+            fs = pfs;
+        }
+    }
+    if (lane == 63) {
+        w_val[wid] = tv;
+        w_fs[wid] = fs;
     }
     __syncthreads();
-    int cur = 0;
-#pragma unroll
-    for (int d = 1; d < kMgThreads; d <<= 1) {
-        float v = t_val[cur][tid];
-        int f = t_flag[cur][tid], sf = t_sf[cur][tid];
-        if (tid >= d && !f) {
-            v = __fadd_rn(t_val[cur][tid - d], v);
-            sf = t_sf[cur][tid - d];
-            f = t_flag[cur][tid - d];
+    if (wid > 0 && !(fs & 1)) {   // the segment began in an earlier wave: add those waves' parts
+        float c = w_val[wid - 1];
+        int32_t cfs = w_fs[wid - 1];
+        for (int32_t k = wid - 2; k >= 0 && !(cfs & 1); --k) {
+            c = __fadd_rn(w_val[k], c);
+            cfs = w_fs[k];
         }
-        t_val[cur ^ 1][tid] = v;
-        t_flag[cur ^ 1][tid] = f;
-        t_sf[cur ^ 1][tid] = sf;
-        cur ^= 1;
-        __syncthreads();
+        tv = __fadd_rn(c, tv);
+        fs = cfs;
     }
+    t_val[tid] = tv;
+    t_sf[tid] = (fs >> 1) & 1;
     // Heads: the thread finished a row started before it -- join it with the tails before.
     // Only the workgroup's first row can have started in an earlier workgroup; its end part
     // goes to the workgroup's record.
@@ -179,8 +195,8 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
         float tot = head;
         bool started_here = false;
         if (tid > 0 && t_row[tid - 1] == first_row) {
-            tot = __fadd_rn(t_val[cur][tid - 1], head);
-            started_here = t_sf[cur][tid - 1] != 0;
+            tot = __fadd_rn(t_val[tid - 1], head);
+            started_here = t_sf[tid - 1] != 0;
         }
         if (started_here) {
             y[first_row] = tot;
@@ -193,8 +209,8 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
     const int32_t t_last = items > 0 ? (items - 1) / kMgIpt : 0;
     if (tid == t_last) {
         rec[blockIdx.x].last_row = open ? r0 + ri : -1;
-        rec[blockIdx.x].last_val = t_val[cur][tid];
-        rec[blockIdx.x].last_fresh = t_sf[cur][tid];
+        rec[blockIdx.x].last_val = t_val[tid];
+        rec[blockIdx.x].last_fresh = t_sf[tid];
     }
     __syncthreads();
     if (tid == 0) {
@@ -204,19 +220,47 @@ __global__ __launch_bounds__(kMgThreads) void spmv_merge_kernel(
 }
 
 // Rows cut between workgroups: workgroup m finished row R (first_row) that began in an earlier
-// one; the workgroups in between lie inside R.  y[R] = start part + middle parts + end part,
-// in workgroup order.
-__global__ void spmv_merge_fixup_kernel(int32_t n_blocks, const MergeRec *__restrict__ rec,
-                                        float *__restrict__ y) {
+// one, the workgroup j holding R's first merge item (diagonal rp[R] + R), whose record's open
+// row is R; the workgroups in between lie inside R.  y[R] = (parts j .. m-1) + end part.  One
+// thread per record: a row over at most kMgLongSpan workgroups (almost every cut row) is joined
+// by its thread in workgroup order; a longer one by the whole wavefront -- lane l adds the
+// parts j + l, j + l + 64, ... in order, then a fixed butterfly joins the lanes -- so a row of
+// 10^8 terms (~5 * 10^4 workgroups) costs ~800 loads per lane instead of 5 * 10^4 in a chain.
+// Which form a row takes depends on the matrix only: deterministic.
+constexpr int64_t kMgLongSpan = 64;
+__global__ __launch_bounds__(256) void spmv_merge_fixup_kernel(int32_t n_blocks, const int32_t *__restrict__ rp,
+                                                                const MergeRec *__restrict__ rec,
+                                                                float *__restrict__ y) {
     const int32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= n_blocks) return;
-    const int32_t R = rec[m].first_row;
-    if (R < 0) return;
-    int32_t j = m - 1;
-    while (j > 0 && !(rec[j].last_row == R && rec[j].last_fresh)) --j;   // the start part
-    float tot = rec[j].last_val;
-    for (int32_t i = j + 1; i < m; ++i) tot = __fadd_rn(tot, rec[i].last_val);
-    y[R] = __fadd_rn(tot, rec[m].first_val);
+    const int32_t lane = threadIdx.x & 63;
+    const int32_t R = m < n_blocks ? rec[m].first_row : -1;
+    const int64_t j = R >= 0 ? ((int64_t)rp[R] + R) / kMgTile : 0;
+    const bool wide = R >= 0 && m - j > kMgLongSpan;
+    if (R >= 0 && !wide) {
+        float tot = rec[j].last_val;
+        for (int64_t i = j + 1; i < m; ++i) tot = __fadd_rn(tot, rec[i].last_val);
+        y[R] = __fadd_rn(tot, rec[m].first_val);
+    }
+    for (uint64_t pend = __ballot(wide); pend != 0; pend &= pend - 1) {   // wave-uniform
+        const int src = __builtin_ctzll(pend);
+        const int32_t mm = __shfl(m, src, 64), RR = __shfl(R, src, 64);
+        const int64_t jj = ((int64_t)rp[RR] + RR) / kMgTile;
+        float part = 0.0f;
+        bool any = false;
+        for (int64_t i = jj + lane; i < mm; i += 64) {
+            const float v = rec[i].last_val;
+            part = any ? __fadd_rn(part, v) : v;
+            any = true;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {   // lane l joins lane l ^ d, the lower lane's part first
+            const float o = __shfl_xor(part, d, 64);
+            const bool oany = __shfl_xor((int)any, d, 64) != 0;
+            if (oany) part = !any ? o : ((lane & d) ? __fadd_rn(o, part) : __fadd_rn(part, o));
+            any = any || oany;
+        }
+        if (lane == 0) y[RR] = __fadd_rn(part, rec[mm].first_val);
+    }
 }
 
 }  // namespace
@@ -237,7 +281,7 @@ hipError_t launch_spmv_merge(int32_t n, int32_t nnz, const int32_t *rp, const in
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(spmv_merge_fixup_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, (int32_t)nb,
-                       rec, y);
+                       rp, rec, y);
     return hipGetLastError();
 }
 

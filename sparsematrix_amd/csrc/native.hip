@@ -159,8 +159,10 @@ __global__ __launch_bounds__(kNatThreads) void native_addmatmat_kernel(
                 xv[k] = 0.0f;
                 if (live) xv[k] = a[off >> 8];
             }
-            const int32_t wi = live ? bit_index(pc & 63, r >> 5) : kDummyWord;
-            atomicOr(&bits[wi], live ? 1u << (r & 31) : 0u);
+            // Dead lanes (fillers, other column groups: most of a sparse panel's entries) issue
+            // no atomic: an OR of 0 into one dummy word from every dead lane serialised them on
+            // one address (r05 PMC: 70 % of the LDS cycles were address/bank conflicts).
+            if (live) atomicOr(&bits[bit_index(pc & 63, r >> 5)], 1u << (r & 31));
             rr[k] = live ? ((pc & 63) << 16) | r : -1;
         }
         __syncthreads();
@@ -348,8 +350,7 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
             xv[k] = 0.0f;
             if (live) xv[k] = x[off >> 8];
         }
-        const int32_t wi = live ? bit_index(pc & 63, r >> 5) : kDummyWord;
-        atomicOr(&bits[wi], live ? 1u << (r & 31) : 0u);
+        if (live) atomicOr(&bits[bit_index(pc & 63, r >> 5)], 1u << (r & 31));   // dead lanes: none (above)
         rr[k] = live ? ((pc & 63) << 16) | r : -1;
     }
     __syncthreads();

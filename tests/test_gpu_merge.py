@@ -192,3 +192,20 @@ def test_merge_rmat24_full_size_vs_oracle(sm):
     assert np.array_equal(bits(got[one]), bits(want[one]))
     _, absum = oracle.csr_spmv_f64(rp.astype(np.int64), ci, va, xh, y0h, 1.0, 0.5)
     assert_terms_close(got, want, absum)
+
+
+def test_merge_one_row_over_thousands_of_workgroups(sm):
+    """a row spanning thousands of workgroups (5 * 10^6 terms, ~2450 slices of 2048
+    items) between short rows: the fixup finds the row's first workgroup from the row pointer
+    and joins the parts in a fixed tree -- deterministic, within the bound."""
+    rng = np.random.default_rng(71)
+    n_rows, n_cols = 3000, 1 << 20
+    lens = rng.integers(0, 20, n_rows).astype(np.int64)
+    lens[1500] = 5_000_000
+    lens[2999] = 300_000
+    rp = np.zeros(n_rows + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate([np.sort(rng.integers(0, n_cols, int(k))) for k in lens]).astype(np.int32)
+    table = rng.uniform(-1, 1, 255).astype(np.float32)
+    va = table[rng.integers(0, 255, ci.size)]
+    _check(sm, rp.astype(np.int32), ci, va, n_cols, 1.0, 0.5, seed=72, want_stage=1)
