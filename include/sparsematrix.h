@@ -262,6 +262,10 @@ typedef struct sm_build_opts {
                                   2-byte slots, 6 bytes per term) when the values form a codebook
                                   and n_cols <= 2^24; the tile gathers x in column order (R-MAT 24:
                                   1.91 -> 1.68 ms), same bits as without.  0 = never (default)  */
+    int32_t host_build;        /* sm_create_from_csr_device: 0 = auto -- the column relabeling and
+                                  the sorted sliced ELL are built on the device where they are
+                                  the only layouts wanted (builddev.hip; the same bytes as the
+                                  host builders); 1 = always on the host                      */
 } sm_build_opts;
 
 SM_API void sm_build_opts_init(sm_build_opts *opts);
@@ -285,6 +289,13 @@ SM_API void sm_destroy(sm_matrix *m);
  * that many bytes.  sm_get_info writes the whole struct of this header. */
 SM_API sm_status sm_get_info(const sm_matrix *m, sm_info *info);
 SM_API sm_status sm_get_info_ex(const sm_matrix *m, sm_info *info, size_t info_bytes);
+/* Diagnostics: 64-bit FNV-1a digests of the device layout arrays, so two builds can be
+ * compared byte for byte (sm_build_opts.host_build): [0] the column relabeling (new column
+ * of every original column, relabeled col_idx), [1] the sorted sliced ELL's structure
+ * (slice offsets and lengths, lane rows and lengths, long rows and their partial offsets),
+ * [2] its slots (column words, values), [3] its codebook.  0 for a part not built.
+ * Synchronises the device. */
+SM_API sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]);
 SM_API int32_t sm_num_rows(const sm_matrix *m);   /* NumRows, sparse-matrix.h:39 */
 SM_API int32_t sm_num_cols(const sm_matrix *m);   /* NumCols, sparse-matrix.h:40 */
 

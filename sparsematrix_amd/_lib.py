@@ -47,7 +47,7 @@ EXPORTS = (
     "sm_multi_last_error", "sm_multi_partition", "sm_multi_unique_id", "sm_multi_create",
     "sm_multi_destroy", "sm_multi_spmv", "sm_multi_spmm", "sm_multi_spmv_batch",
     "sm_multi_allgather", "sm_multi_set_timing", "sm_multi_last_times", "sm_multi_create_with",
-    "sm_debug_seed_handoff",
+    "sm_debug_seed_handoff", "sm_layout_digest",
 )
 
 SM_UNIQUE_ID_BYTES = 128
@@ -94,6 +94,7 @@ class SmBuildOpts(C.Structure):
         ("sell_sigma", C.c_int64), ("relabel", C.c_int32), ("tile_nnz", C.c_int32),
         ("ccsell", C.c_int32), ("ccsell_chunk_log2", C.c_int32), ("hot_cols", C.c_int32),
         ("exact_sell", C.c_int32), ("band_slab0_permille", C.c_int32), ("merge_stage", C.c_int32),
+        ("host_build", C.c_int32),
     ]
 
 
@@ -143,6 +144,7 @@ def _declare(L):
         "sm_destroy": ([_vp], None),
         "sm_get_info": ([_vp, C.POINTER(SmInfo)], C.c_int),
         "sm_get_info_ex": ([_vp, C.POINTER(SmInfo), C.c_size_t], C.c_int),
+        "sm_layout_digest": ([_vp, C.POINTER(C.c_uint64)], C.c_int),
         "sm_num_rows": ([_vp], _i32),
         "sm_num_cols": ([_vp], _i32),
         "sm_copy_ref_stream": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),

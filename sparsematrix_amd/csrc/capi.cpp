@@ -74,6 +74,7 @@ hipError_t dev_alloc(T **p, int64_t count, int64_t &acct) {
 }
 
 void free_xband_dev(XbandDev &h) {
+    (void)hipFree(h.d_late);
     (void)hipFree(h.d_chunk_start);
     (void)hipFree(h.d_word);
     (void)hipFree(h.d_val);
@@ -109,13 +110,7 @@ void free_device(sm_matrix *m) {
     (void)hipFree(m->plan.d_long_ptr);
     (void)hipFree(m->plan.d_chunks);
     (void)hipFree(m->plan.d_partials);
-    (void)hipFree(m->plan.xb.d_chunk_start);
-    (void)hipFree(m->plan.xb.d_word);
-    (void)hipFree(m->plan.xb.d_val);
-    (void)hipFree(m->plan.xb.d_partials);
-    (void)hipFree(m->plan.xb.d_tickets);
-    (void)hipFree(m->plan.xb.d_band_clo);
-    (void)hipFree(m->plan.xb.d_table);
+    free_xband_dev(m->plan.xb);
     (void)hipFree(m->plan.d_perm);
     (void)hipFree(m->plan.d_rcol);
     (void)hipFree(m->plan.d_xperm);
@@ -192,6 +187,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
         r.exact_sell = d.exact_sell;
         r.band_slab0_permille = d.band_slab0_permille;
         r.merge_stage = d.merge_stage;
+        r.host_build = d.host_build;
     }
     if (const char *e = dev_env("SM_XBAND")) r.layout = atoi(e) ? SM_LAYOUT_BANDS : SM_LAYOUT_NO_BANDS;
     if (const char *e = dev_env("SM_XBAND_KIND")) {
@@ -216,6 +212,7 @@ BuildOpts resolve_opts(const sm_build_opts *o) {
     if (const char *e = dev_env("SM_CCSELL_CHUNK")) r.ccsell_chunk_log2 = atoi(e);
     if (const char *e = dev_env("SM_HOT_COLS")) r.hot_cols = atoi(e);
     if (const char *e = dev_env("SM_MERGE_STAGE")) r.merge_stage = atoi(e);
+    if (const char *e = dev_env("SM_HOST_BUILD")) r.host_build = atoi(e);
     return r;
 }
 
@@ -244,6 +241,7 @@ sm_status check_opts(const sm_build_opts *o) {
     if (r.band_slab0_permille != 0 && (r.band_slab0_permille < 500 || r.band_slab0_permille > 1000))
         return fail(SM_ERR_INVALID_ARG, "band_slab0_permille must be 0 or 500..1000");
     if (r.merge_stage != 0 && r.merge_stage != 1) return fail(SM_ERR_INVALID_ARG, "merge_stage must be 0 or 1");
+    if (r.host_build != 0 && r.host_build != 1) return fail(SM_ERR_INVALID_ARG, "host_build must be 0 or 1");
     return SM_OK;
 }
 
@@ -389,6 +387,8 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)bh.n_slabs * ps, m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)bh.n_blocks, m->device_bytes));
         SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)bh.n_blocks * 4 * sizeof(int32_t)));
+        SM_TRY_HIP(dev_alloc(&d.d_late, ntile * kB2LateWords, m->device_bytes));
+        SM_TRY_HIP(hipMemcpy(d.d_late, bh.late.data(), (size_t)ntile * kB2LateWords * 4, hipMemcpyHostToDevice));
     }
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, bh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
                          hipMemcpyHostToDevice));
@@ -1115,6 +1115,26 @@ hipError_t with_scratch(const sm_matrix *m, hipStream_t s, bool needed, F &&laun
 bool native_scratch(const NativeDev &nd) { return nd.d_lists && nd.max_panel_batches > kNatFusedBatches; }
 }  // namespace
 
+namespace {
+// FNV-1a over device arrays (sm_layout_digest).
+struct Fnv {
+    uint64_t h = 1469598103934665603ull;
+    void add(const void *p, size_t n) {
+        const uint8_t *b = static_cast<const uint8_t *>(p);
+        for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    }
+};
+template <class T>
+sm_status fnv_dev(Fnv &f, const T *d, int64_t n) {
+    if (!d || n <= 0) return SM_OK;
+    std::vector<T> h((size_t)n);
+    const hipError_t e = hipMemcpy(h.data(), d, (size_t)n * sizeof(T), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "sm_layout_digest");
+    f.add(h.data(), h.size() * sizeof(T));
+    return SM_OK;
+}
+}  // namespace
+
 extern "C" {
 
 const char *sm_version(void) { return "sparsematrix_amd 0.2 (gfx950)"; }
@@ -1454,12 +1474,32 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
     }
     st = upload_plan(m.get(), rp.data());
     const bool xband = want_xband(m.get());
+    // The column relabeling and the sorted sliced ELL on the device (builddev.hip) where they
+    // are all this matrix wants: no band layout, sweep, hot split, merge staging copy, windowed
+    // sort or exact sliced ELL, and no column-chunked ELL once the relabeling is decided (its
+    // builder runs on the host).  R-MAT 24: the host path took 5.4 s.
+    bool dev_done = false;
+    if (st == SM_OK && m->opts.host_build == 0 && !xband && !want_sweep(m.get()) && m->opts.hot_cols <= 0 &&
+        !want_merge_stage(m.get()) && m->opts.sell_sigma == 0 && m->opts.sell_streams <= 1 &&
+        m->opts.exact_sell != 1) {
+        hipError_t eb = hipSuccess;
+        int rc = 0;
+        if (want_relabel_size(m.get())) rc = devbuild_relabel(m.get(), m->opts.relabel != 1, s, eb);
+        if (rc == 0 && !want_ccsell(m.get())) {
+            if (want_sell(m.get())) {
+                const int32_t max_len = m->opts.sell_max_len > 0 ? m->opts.sell_max_len : kSellMaxLen;
+                rc = devbuild_sell(m.get(), max_len, m->opts.sell_codebook != 0, s, eb);
+            }
+            dev_done = rc == 0;
+        }
+        if (rc != 0) st = hip_fail(eb, "device layout builder");
+    }
     const bool maybe_sell = m->opts.sell != 0 && nnz > 0;
     // The band / sell builders run on the host (band2.cpp, xband.cpp, sell.cpp): the
     // columns come down for any of them, the values only for the layout that stores
     // them (4 + 4 bytes per term over PCIe once, at creation).
-    if (st == SM_OK && (xband || want_relabel_size(m.get()) || maybe_sell || want_sweep(m.get()) ||
-                        want_merge_stage(m.get()))) {
+    if (st == SM_OK && !dev_done &&
+        (xband || want_relabel_size(m.get()) || maybe_sell || want_sweep(m.get()) || want_merge_stage(m.get()))) {
         std::vector<int32_t> ch((size_t)nnz);
         std::vector<float> vh;
         auto values = [&]() -> sm_status {
@@ -1555,6 +1595,50 @@ sm_status sm_get_info_ex(const sm_matrix *m, sm_info *out, size_t info_bytes) {
     }
     // Only the bytes the caller's struct has (an older, shorter sm_info stays valid).
     memcpy(out, &full, std::min(info_bytes, sizeof(full)));
+    return SM_OK;
+}
+
+sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]) {
+    if (!m || !digest) return fail(SM_ERR_INVALID_ARG, "null argument");
+    DeviceGuard g(m->device);
+    if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+    for (int k = 0; k < 4; k++) digest[k] = 0;
+    const Plan &p = m->plan;
+    sm_status st = SM_OK;
+    if (p.n_relabel > 0) {
+        Fnv f;
+        if ((st = fnv_dev(f, p.d_perm, p.n_relabel)) != SM_OK) return st;
+        if ((st = fnv_dev(f, p.d_rcol, m->nnz)) != SM_OK) return st;
+        digest[0] = f.h;
+    }
+    const SellDev &d = p.sell;
+    if (d.n_slices > 0) {
+        std::vector<int64_t> off((size_t)d.n_slices);
+        std::vector<int32_t> len((size_t)d.n_slices);
+        SM_TRY_HIP(hipMemcpy(off.data(), d.d_off, off.size() * 8, hipMemcpyDeviceToHost));
+        SM_TRY_HIP(hipMemcpy(len.data(), d.d_len, len.size() * 4, hipMemcpyDeviceToHost));
+        const int64_t padded = off.back() + (int64_t)len.back() * kSellLanes;
+        Fnv f;
+        f.add(off.data(), off.size() * 8);
+        f.add(len.data(), len.size() * 4);
+        if ((st = fnv_dev(f, d.d_row, d.n_slices * kSellLanes)) != SM_OK) return st;
+        if ((st = fnv_dev(f, d.d_row_len, d.n_slices * kSellLanes)) != SM_OK) return st;
+        f.add(&d.n_long, 4);
+        f.add(&d.max_len, 4);
+        if ((st = fnv_dev(f, d.d_long_rows, d.n_long)) != SM_OK) return st;
+        if ((st = fnv_dev(f, d.d_long_ptr, d.n_long + 1)) != SM_OK) return st;
+        digest[1] = f.h;
+        Fnv c;
+        if ((st = fnv_dev(c, d.d_col, padded + 32 * kSellLanes)) != SM_OK) return st;
+        if ((st = fnv_dev(c, d.d_val, d.d_val ? padded + 32 * kSellLanes : 0)) != SM_OK) return st;
+        digest[2] = c.h;
+        if (d.d_table) {
+            Fnv t;
+            if ((st = fnv_dev(t, d.d_table, d.table_size)) != SM_OK) return st;
+            t.add(&d.table_size, 4);
+            digest[3] = t.h;
+        }
+    }
     return SM_OK;
 }
 

@@ -56,6 +56,7 @@ struct BuildOpts {
     int32_t exact_sell = 0;   // 0 auto, 1 always, -1 never (sm_build_opts.exact_sell)
     int32_t band_slab0_permille = 0;   // 0 auto (sm_build_opts.band_slab0_permille)
     int32_t merge_stage = 0;           // sm_build_opts.merge_stage
+    int32_t host_build = 0;            // sm_build_opts.host_build
 };
 
 // Row tile: rows [r0, r1) whose terms fit one LDS tile.  flags bit0: the tile
@@ -87,6 +88,9 @@ struct XbandDev {
     // band2 kind (band2.cpp): d_chunk_start = tile -> first band (n_tiles + 1), d_word =
     // the lane-interleaved entries (4096 per band), d_band_clo = each band's first column.
     int32_t *d_band_clo = nullptr;
+    // band2 / cband with several slabs: per tile the float4s of rows its last band touches
+    // (xband.h kB2LateWords) -- the others are published during that band.
+    uint32_t *d_late = nullptr;
     // cband kind: the codebook (table_size <= 255 floats) the entries' ids index.
     float *d_table = nullptr;
     int32_t table_size = 0;
@@ -299,6 +303,12 @@ struct EncodeResult;
 int encode_csr_ref_device(const int32_t *d_rp, const int32_t *d_col, const float *d_val, const uint8_t *d_ids,
                           int64_t n_rows, int64_t n_cols, int64_t nnz, const float *table,
                           int32_t table_size, EncodeResult &out, hipStream_t s, hipError_t &err);
+// Device builders (builddev.hip) on a matrix whose CSR is on the device: the column
+// relabeling (check_skew: only if the top 1/16 of the columns hold >= 40 % of the terms) and
+// the sorted sliced ELL (codebook form when the values allow), the bytes upload_relabel and
+// upload_sell build on the host.  0 built or declined as the host would, -5 HIP error (err).
+int devbuild_relabel(sm_matrix *m, bool check_skew, hipStream_t s, hipError_t &err);
+int devbuild_sell(sm_matrix *m, int32_t max_len, bool codebook, hipStream_t s, hipError_t &err);
 hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
                            const int32_t *col, int32_t *d_flag, hipStream_t s);
 // Dense decode: out is zeroed by the caller.  b_layout: out[row*stride+col]

@@ -199,6 +199,13 @@ class SparseMatrix:
         check(self._L.sm_get_info_ex(self._require(), C.byref(inf), C.sizeof(inf)), "sm_get_info")
         return {k: getattr(inf, k) for k, _ in SmInfo._fields_}
 
+    def layout_digest(self) -> tuple:
+        """sm_layout_digest: FNV-1a digests of the relabeling, the sliced ELL's structure, its
+        slots and its codebook (0 where not built)."""
+        d = (C.c_uint64 * 4)()
+        check(self._L.sm_layout_digest(self._require(), d), "sm_layout_digest")
+        return tuple(int(v) for v in d)
+
     @property
     def n_rows(self) -> int:
         return self.info()["n_rows"]

@@ -1,0 +1,119 @@
+"""Device layout builders (sparsematrix_amd/csrc/builddev.hip): from a
+device CSR the column relabeling and the sorted sliced ELL are built on the GPU.  Every case
+builds the same matrix both ways (sm_build_opts.host_build = 0 / 1) and checks the layouts byte
+for byte (sm_layout_digest: relabeling, slice structure, slots, codebook), the reported layout
+and the SpMV results bit for bit -- and, for the sliced ELL's rows of <= 2048 terms, the
+reference's order (oracle.csr_spmv: kernel.cc:780-796)."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+from gpu_util import assert_terms_close, bits, to_host, torch_dev
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("sell_slices", "sell_codebook", "col_relabel", "n_long_rows", "max_row_nnz", "device_bytes", "has_xband",
+        "ccsell_chunks")
+
+
+@pytest.fixture(scope="module")
+def sm():
+    torch_dev()
+    oracle.build()
+    import sparsematrix_amd
+    sparsematrix_amd.load()
+    return sparsematrix_amd
+
+
+def _both(sm, rp, ci, va, n_cols, opts=None):
+    torch = torch_dev()
+    out = []
+    for hb in (0, 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(opts or {}, host_build=hb))
+        torch.cuda.synchronize()
+        out.append((M, time.perf_counter() - t0))
+    (D, td), (H, th) = out
+    di, hi = D.info(), H.info()
+    assert {k: di[k] for k in KEYS} == {k: hi[k] for k in KEYS}, (di, hi)
+    assert D.layout_digest() == H.layout_digest(), (D.layout_digest(), H.layout_digest())
+    print(f"build: device {td:.2f} s, host {th:.2f} s", {k: di[k] for k in KEYS[:5]})
+    return D, H, di
+
+
+def _spmv_both(D, H, n_rows, n_cols, seed):
+    torch = torch_dev()
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.rand(n_cols, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n_rows, device="cuda", generator=g) * 2 - 1
+    yd, yh = y0.clone(), y0.clone()
+    D.spmv(x, yd, 1.3, 0.5)
+    H.spmv(x, yh, 1.3, 0.5)
+    assert torch.equal(yd.view(torch.int32), yh.view(torch.int32))
+    return to_host(x), to_host(y0), to_host(yd)
+
+
+def _rmat(scale, seed):
+    import sparsematrix_amd.synth as synth
+    return synth.rmat_device(scale, 16, seed=seed)
+
+
+def test_devbuild_rmat18_relabel_codebook_vs_oracle(sm):
+    """R-MAT scale 18: relabeled columns, codebook words, rows over 2048 terms cut in
+    segments; rows of <= 2048 terms bit-identical to the reference order."""
+    rp, ci, va = _rmat(18, 7)
+    n = 1 << 18
+    D, H, info = _both(sm, rp, ci, va, n)
+    assert info["col_relabel"] == 1 and info["sell_codebook"] == 1 and info["sell_slices"] > 0, info
+    xh, y0h, got = _spmv_both(D, H, n, n, 3)
+    rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
+    want = oracle.csr_spmv(rph, cih, vah, xh, y0h, 1.3, 0.5)
+    short = np.diff(rph.astype(np.int64)) <= 2048
+    assert np.array_equal(bits(got[short]), bits(want[short]))
+    _, absum = oracle.csr_spmv_f64(rph.astype(np.int64), cih, vah, xh, y0h, 1.3, 0.5)
+    assert_terms_close(got, want, absum)
+
+
+def test_devbuild_plain_values_short_segments(sm):
+    """Values beyond a codebook (plain column + value slots), a 64-term segment cap (many long
+    rows: sm_build_opts.sell_max_len) and relabeling forced."""
+    torch = torch_dev()
+    rp, ci, _ = _rmat(16, 9)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    va = torch.rand(ci.numel(), device="cuda", generator=g) * 2 - 1
+    n = 1 << 16
+    D, H, info = _both(sm, rp, ci, va, n, dict(sell_max_len=64, relabel=1))
+    assert info["sell_codebook"] == 0 and info["n_long_rows"] > 0, info
+    _spmv_both(D, H, n, n, 4)
+
+
+def test_devbuild_codebook_edges_and_no_relabel(sm):
+    """Exactly 255 and 256 distinct values (codebook / plain), empty rows, and a uniform matrix
+    whose relabeling is declined (not skewed): the sliced ELL over the original columns."""
+    torch = torch_dev()
+    rng = np.random.default_rng(11)
+    n_rows, n_cols = 40000, 1 << 20
+    lens = rng.integers(0, 40, n_rows)
+    lens[::7] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, int(k), replace=False)) for k in lens]).astype(np.int32)
+    for k in (255, 256):
+        table = rng.uniform(-1, 1, k).astype(np.float32)
+        va = table[np.arange(ci.size) % k]   # every value present
+        dev = [torch.from_numpy(a).cuda() for a in (rp, ci, va)]
+        D, H, info = _both(sm, *dev, n_cols, dict(layout="no_bands"))
+        assert info["col_relabel"] == 0 and info["sell_codebook"] == (1 if k == 255 else 0), info
+        _spmv_both(D, H, n_rows, n_cols, 6)
+
+
+def test_devbuild_config4_rmat24_full_size(sm):
+    """BASELINE config 4 exactly as bench.py builds it (R-MAT scale 24, seed 4): the device
+    build is byte-identical to the host build and much faster (printed)."""
+    rp, ci, va = _rmat(24, 4)
+    n = 1 << 24
+    D, H, info = _both(sm, rp, ci, va, n)
+    assert info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
+    _spmv_both(D, H, n, n, 8)
