@@ -27,7 +27,6 @@ namespace {
 struct TileOut {
     std::vector<int32_t> clo;
     std::vector<uint32_t> ent;
-    std::vector<uint32_t> late;   // kB2LateWords: the float4s of rows the last band touches
     int64_t terms = 0;
     bool ok = true;
 };
@@ -423,17 +422,6 @@ void build_tile(const int32_t *rp, const int32_t *col, const float *val, const u
     }
     for (int64_t r = 0; r < nr; r++)
         if (cur[(size_t)r] != end[(size_t)r]) out.ok = false;   // unsorted columns
-    // The rows of the tile's last band (segs still holds them): their sums change in that band,
-    // every other row is final after the band before it (xband.h b2_late_bit).
-    // Blocks of more than 16384 rows (the builder's tall geometries, not run by the kernel) get
-    // an all-ones mask: nothing published early.
-    const bool fits = nr <= 4 * 64 * 64;
-    out.late.assign(kB2LateWords, fits ? 0u : ~0u);
-    if (!out.clo.empty() && fits)
-        for (const Seg &g : segs) {
-            const int32_t f = g.rl >> 2;
-            out.late[(size_t)b2_late_word(f)] |= 1u << b2_late_bit(f);
-        }
 }
 
 }  // namespace
@@ -505,9 +493,7 @@ bool band2_build(const int32_t *rp, const int32_t *col, const float *val, int64_
     out.n_bands = nb;
     out.band_clo.reserve((size_t)nb);
     out.ent.reserve((size_t)(nb * band_words));
-    out.late.reserve((size_t)ntile * kB2LateWords);
     for (auto &t : tiles) {
-        out.late.insert(out.late.end(), t.late.begin(), t.late.end());
         out.band_clo.insert(out.band_clo.end(), t.clo.begin(), t.clo.end());
         out.ent.insert(out.ent.end(), t.ent.begin(), t.ent.end());
         std::vector<uint32_t>().swap(t.ent);

@@ -74,7 +74,6 @@ hipError_t dev_alloc(T **p, int64_t count, int64_t &acct) {
 }
 
 void free_xband_dev(XbandDev &h) {
-    (void)hipFree(h.d_late);
     (void)hipFree(h.d_chunk_start);
     (void)hipFree(h.d_word);
     (void)hipFree(h.d_val);
@@ -387,8 +386,6 @@ static sm_status build_band2(sm_matrix *m, XbandDev &d, int64_t n_rows, int64_t 
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)bh.n_slabs * ps, m->device_bytes));
         SM_TRY_HIP(dev_alloc(&d.d_tickets, 4 * (int64_t)bh.n_blocks, m->device_bytes));
         SM_TRY_HIP(hipMemset(d.d_tickets, 0, (size_t)bh.n_blocks * 4 * sizeof(int32_t)));
-        SM_TRY_HIP(dev_alloc(&d.d_late, ntile * kB2LateWords, m->device_bytes));
-        SM_TRY_HIP(hipMemcpy(d.d_late, bh.late.data(), (size_t)ntile * kB2LateWords * 4, hipMemcpyHostToDevice));
     }
     SM_TRY_HIP(hipMemcpy(d.d_chunk_start, bh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
                          hipMemcpyHostToDevice));
@@ -1626,7 +1623,7 @@ sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]) {
         f.add(&d.n_long, 4);
         f.add(&d.max_len, 4);
         if ((st = fnv_dev(f, d.d_long_rows, d.n_long)) != SM_OK) return st;
-        if ((st = fnv_dev(f, d.d_long_ptr, d.n_long + 1)) != SM_OK) return st;
+        if ((st = fnv_dev(f, d.d_long_ptr, d.n_long > 0 ? d.n_long + 1 : 0)) != SM_OK) return st;
         digest[1] = f.h;
         Fnv c;
         if ((st = fnv_dev(c, d.d_col, padded + 32 * kSellLanes)) != SM_OK) return st;

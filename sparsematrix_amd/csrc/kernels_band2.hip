@@ -20,10 +20,10 @@
 // consecutive lanes by DPP, its last lane writes; no two lanes touch one row in a round, no
 // atomics).  Summation order: bands ascend in column, a row's terms inside a band ascend in
 // column, so inside a tile every row is summed in the reference's order (kernel.cc:780-796,
-// per output ascending column, kernel.cc:791 for the term); slab 0 starts from beta*y,
-// later slabs from -0.0, and the slab sums are added in slab order by the slab hand-off
-// (xband_dev.h slab_handoff_epoch) -- bit-identical to the reference with one slab, within
-// the Sum|terms| bound otherwise, deterministic always.
+// per output ascending column, kernel.cc:791 for the term).  One slab: the tile starts from
+// beta*y -- bit-identical to the reference.  Several: every slab tile starts from -0.0 and the
+// slab hand-off (xband_dev.h slab_handoff_epoch, beta-last) forms beta*y and adds the slab
+// sums in slab order -- within the Sum|terms| bound, deterministic.
 //
 // The variants measured slower over rounds 2-5 (tall, wide3, half2 and dma3-tall
 // geometries, several loader waves, x by LDS-DMA in the wide geometry, early entry loads,
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     const int32_t *__restrict__ tile_band_start, const int32_t *__restrict__ band_clo,
     const uint32_t *__restrict__ ent, const float *__restrict__ table, int32_t table_size,
     const float *__restrict__ x, float *__restrict__ y, float *__restrict__ partials,
-    int32_t *__restrict__ ctl, float alpha, float beta, const uint32_t *__restrict__ late) {
+    int32_t *__restrict__ ctl, float alpha, float beta) {
     static_assert(GEO == 0 || GEO == 4, "wide or dma3");
     constexpr bool kLd = GEO == 4;   // dma3: wave kLdWave stages x, the others apply
     constexpr B2Geom G = kLd ? (CB ? kB2Dma3Cb : kB2Dma3B2) : kB2Wide;
@@ -357,21 +357,12 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
     // back edge leaves them.
     [[maybe_unused]] float4 X[AX][XV];
     EV E[AE];
-    // Early publish (xband.h kB2LateWords; beta-last hand-off, dma3): the loader's two words of
-    // the tile's late-row mask -- bit k of word j: float4 lane + 64 (32 j + k) of the block's rows
-    // is touched by the last band.
-    const bool early = kLd && SM_B2_BL && SM_B2_EARLY && late != nullptr && n_slabs > 1 && nb > 0;
-    uint32_t late_w0 = 0, late_w1 = 0;
     if constexpr (kLd) {
 #pragma unroll
         for (int v = 0; v < AE; ++v) E[v] = load_e(v);
         if (wid == kLdWave) {   // windows 0 and 1; waited for (with everything) below
             if (nb > 0) dma_win(clg[0], 0);
             if (nb > 1) dma_win(clg[1], 1);
-            if (early) {
-                late_w0 = late[(int64_t)t * kB2LateWords + 2 * lane];
-                late_w1 = late[(int64_t)t * kB2LateWords + 2 * lane + 1];
-            }
         }
     } else {
 #pragma unroll
@@ -467,30 +458,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
             // wait for the whole DMA queue before reading it).
             int32_t c_next = nb > 2 ? clg[2] : 0;
             __builtin_amdgcn_s_setprio(kLoaderPrio);
-            // The last band (q = nb - 1) has no window to stage: the rows it does not touch are
-            // final (every wave passed band nb - 2's barrier), so the loader publishes them now,
-            // write-through, while the others apply it -- the epilogue's burst keeps only the last
-            // band's rows (xband_dev.h publish_rows_rest; drained before the arrival add).
-            auto publish_early = [&]() {
-                const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;
-                const __amdgpu_buffer_rsrc_t o_src = rsrc(partials + (int64_t)slab * ps + r0, (uint64_t)nr * 4);
-                const int32_t part = ((nr + n_slabs - 1) / n_slabs + 3) & ~3;
-                const int32_t own_lo = min(slab * part, nr), own_hi = min((slab + 1) * part, nr);
-#pragma unroll 4
-                for (int k = 0; k < 64; ++k) {
-                    const int32_t f = lane + 64 * k;
-                    const uint32_t w = k < 32 ? late_w0 : late_w1;
-                    const bool own = 4 * f >= own_lo && 4 * f < own_hi;
-                    if (((w >> (k & 31)) & 1u) == 0u && !own && 4 * f + 4 <= nr) {
-                        const float4 v = *reinterpret_cast<const float4 *>(&yacc[4 * f]);
-                        const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                                         __float_as_uint(v.w)};
-                        __builtin_amdgcn_raw_buffer_store_b128(u, o_src, 16u * (uint32_t)f, 0, kAuxSc1);
-                    }
-                }
-            };
             for (int32_t q = 0; q < nb; ++q) {
-                if (early && q == nb - 1) publish_early();
                 if (q + 2 < nb) {
                     const int32_t c = c_next;
                     const int32_t qn = __builtin_amdgcn_readfirstlane(q + 3);
@@ -581,7 +549,7 @@ __global__ __launch_bounds__(kB2Threads) void spmv_band2_kernel(
 #endif
     slab_handoff_epoch<kB2Threads, SM_B2_BL != 0>(yacc, ctl + (int64_t)b * kCtlWords, s_word, y, partials,
                                                   n_rows, r0, nr, slab, n_slabs, y_vec, old_started, snap, beta,
-                                                  ts, early ? late + (int64_t)t * kB2LateWords : nullptr);
+                                                  ts);
     flush_prof();
 }
 
@@ -593,7 +561,7 @@ hipError_t launch_prof(int prof, dim3 grid, hipStream_t s, const XbandDev &xb, i
 #define SM_B2P(P)                                                                                   \
     hipLaunchKernelGGL((spmv_band2_kernel<true, GEO, P>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols, \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.d_late)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
     if (prof == 1) {
         if (GEO != 4) return hipErrorInvalidValue;
         unsigned long long h[8] = {};
@@ -692,7 +660,7 @@ hipError_t launch_spmv_band2(const XbandDev &xb, int32_t n_rows, int32_t n_cols,
 #define SM_B2(C, T)                                                                                 \
     hipLaunchKernelGGL((spmv_band2_kernel<C, T, 0>), grid, dim3(kB2Threads), 0, s, n_rows, n_cols,    \
                        xb.block_rows, xb.n_slabs, xb.d_chunk_start, xb.d_band_clo, xb.d_word,          \
-                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta, xb.d_late)
+                       xb.d_table, xb.table_size, x, y, xb.d_partials, xb.d_tickets, alpha, beta)
     if (dma3) {
         if (cb) SM_B2(true, 4); else SM_B2(false, 4);
     } else {

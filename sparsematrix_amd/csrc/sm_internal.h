@@ -88,9 +88,6 @@ struct XbandDev {
     // band2 kind (band2.cpp): d_chunk_start = tile -> first band (n_tiles + 1), d_word =
     // the lane-interleaved entries (4096 per band), d_band_clo = each band's first column.
     int32_t *d_band_clo = nullptr;
-    // band2 / cband with several slabs: per tile the float4s of rows its last band touches
-    // (xband.h kB2LateWords) -- the others are published during that band.
-    uint32_t *d_late = nullptr;
     // cband kind: the codebook (table_size <= 255 floats) the entries' ids index.
     float *d_table = nullptr;
     int32_t table_size = 0;

@@ -148,22 +148,8 @@ struct Band2Host {
     std::vector<int32_t> tile_band_start;   // n_blocks * n_slabs + 1 (tile t = b * S + s)
     std::vector<int32_t> band_clo;          // first column of each band's window (multiple of 4)
     std::vector<uint32_t> ent;              // 4096 per band
-    std::vector<uint32_t> late;             // kB2LateWords per tile (b2_late_word)
     int64_t real_terms = 0;                 // for the padding report
 };
-
-// Early publish (band2 / cband with several slabs, dma3): a tile's rows that its last band does
-// not touch are final one band before the loop ends, so the loader wave -- idle then -- publishes
-// them during that band and only the last band's rows wait for the epilogue
-// (kernels_band2.hip; the hand-off's write-through burst, profiles/r06_handoff_timeline.txt).
-// One bit per float4 of the block's rows (<= 16384 rows: 4096 float4), laid out so that lane
-// l of a wave holds the bits of float4s l, l + 64, ..., l + 4032 in words 2 l and 2 l + 1.
-#ifndef SM_B2_EARLY
-#define SM_B2_EARLY 1   // 0: everything published in the epilogue (development A/B)
-#endif
-constexpr int kB2LateWords = 128;
-inline int32_t b2_late_word(int32_t f) { return 2 * (f & 63) + ((f >> 6) >> 5); }
-inline int32_t b2_late_bit(int32_t f) { return (f >> 6) & 31; }
 
 // Returns false when the layout does not apply: unsorted columns or size limits
 // (a row segment longer than 14 terms -- 63 with ids -- cuts the band instead).

@@ -83,35 +83,6 @@ __device__ __forceinline__ void publish_rows(const float *yacc, float *out, bool
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yacc[i]), o_src, 4u * i, 0, kAuxSc1);
 }
 
-// Early publish (xband.h kB2LateWords): float4 f of the block's rows was published during the
-// tile's last band when it lies outside the own part [own_lo, own_hi), holds 4 whole rows and
-// none of them is touched by that band.  late: the tile's kB2LateWords words (nullptr: none).
-__device__ __forceinline__ bool published_early(const uint32_t *late, int32_t f, int32_t own_lo, int32_t own_hi,
-                                                int32_t nr) {
-    if (late == nullptr || 4 * f + 4 > nr || (4 * f >= own_lo && 4 * f < own_hi)) return false;
-    const uint32_t w = late[2 * (f & 63) + ((f >> 6) >> 5)];
-    return ((w >> ((f >> 6) & 31)) & 1u) == 0u;
-}
-
-// publish_rows less the float4s published early (the vector loop covers whole float4s only).
-template <int THREADS>
-__device__ __forceinline__ void publish_rows_rest(const float *yacc, float *out, int32_t lo, int32_t hi, int32_t nr,
-                                                  const uint32_t *late, int32_t own_lo, int32_t own_hi) {
-    if (lo >= hi) return;
-    const __amdgpu_buffer_rsrc_t o_src = rsrc(out, (uint64_t)nr * 4);
-    const int32_t tid = threadIdx.x;
-    const int32_t hv = lo + ((hi - lo) & ~3);   // lo is a multiple of 4
-    for (int32_t i = lo + 4 * tid; i < hv; i += 4 * THREADS) {
-        if (published_early(late, i >> 2, own_lo, own_hi, nr)) continue;
-        const float4 v = *reinterpret_cast<const float4 *>(&yacc[i]);
-        const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                         __float_as_uint(v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(u, o_src, 4u * i, 0, kAuxSc1);
-    }
-    for (int32_t i = hv + tid; i < hi; i += THREADS)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yacc[i]), o_src, 4u * i, 0, kAuxSc1);
-}
-
 // y[lo, hi) = P_0 + ... + P_{S-1} in slab order; P_me from LDS, the others from
 // y (slab 0) and partials[s-1] with sc1 loads, up to 4 slabs' loads in flight.
 template <int THREADS>
@@ -316,8 +287,7 @@ template <int THREADS, bool BL>
 __device__ __forceinline__ void slab_handoff_epoch(const float *yacc, int32_t *ctl, int32_t *s_word, float *y,
                                    float *partials, int32_t n_rows, int32_t r0, int32_t nr,
                                    int32_t slab, int32_t n_slabs, bool y_vec, uint64_t old_started,
-                                   uint64_t snapshot, float beta, unsigned long long *ts,
-                                   const uint32_t *late = nullptr) {
+                                   uint64_t snapshot, float beta, unsigned long long *ts) {
     const int32_t tid = threadIdx.x;
     const int64_t ps = ((int64_t)n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
     // BL: every slab publishes into partials[slab]; otherwise slab 0 into y, s >= 1 into partials[s-1].
@@ -348,20 +318,13 @@ __device__ __forceinline__ void slab_handoff_epoch(const float *yacc, int32_t *c
     const bool committed = s_word[0] != 0;
     const uint32_t g = (uint32_t)s_word[3];   // the generation's parity
     int32_t *arrive = ctl + 2 + g;
-    if (BL && late != nullptr) {   // the loader published the rest during the last band
-        if (committed) {
-            publish_rows_rest<THREADS>(yacc, outp, 0, part_lo(slab), nr, late, part_lo(slab), part_hi(slab));
-            publish_rows_rest<THREADS>(yacc, outp, part_hi(slab), nr, nr, late, part_lo(slab), part_hi(slab));
-        } else {
-            publish_rows_rest<THREADS>(yacc, outp, 0, nr, nr, late, part_lo(slab), part_hi(slab));
-        }
-    } else if (committed) {   // the own part stays in LDS
+    if (committed) {   // the own part stays in LDS
         publish_rows<THREADS>(yacc, outp, vec_out, 0, part_lo(slab), nr);
         publish_rows<THREADS>(yacc, outp, vec_out, part_hi(slab), nr, nr);
     } else {
         publish_rows<THREADS>(yacc, outp, vec_out, 0, nr, nr);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its own and its early stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stamp(0);
     if (tid == 0) {

@@ -66,7 +66,7 @@ def test_devbuild_rmat18_relabel_codebook_vs_oracle(sm):
     segments; rows of <= 2048 terms bit-identical to the reference order."""
     rp, ci, va = _rmat(18, 7)
     n = 1 << 18
-    D, H, info = _both(sm, rp, ci, va, n)
+    D, H, info = _both(sm, rp, ci, va, n, dict(layout="no_bands", relabel=1))   # AUTO: bands here
     assert info["col_relabel"] == 1 and info["sell_codebook"] == 1 and info["sell_slices"] > 0, info
     xh, y0h, got = _spmv_both(D, H, n, n, 3)
     rph, cih, vah = rp.cpu().numpy(), ci.cpu().numpy(), va.cpu().numpy()
@@ -85,7 +85,7 @@ def test_devbuild_plain_values_short_segments(sm):
     g = torch.Generator(device="cuda").manual_seed(5)
     va = torch.rand(ci.numel(), device="cuda", generator=g) * 2 - 1
     n = 1 << 16
-    D, H, info = _both(sm, rp, ci, va, n, dict(sell_max_len=64, relabel=1))
+    D, H, info = _both(sm, rp, ci, va, n, dict(layout="no_bands", sell_max_len=64, relabel=1))
     assert info["sell_codebook"] == 0 and info["n_long_rows"] > 0, info
     _spmv_both(D, H, n, n, 4)
 
