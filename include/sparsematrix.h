@@ -25,7 +25,8 @@
  * bit-identical to the reference CPU kernel.  SM_ALGO_XBAND keeps that order for
  * every row on the exact band layout (sm_info.has_xband == 1, or any layout with
  * xband_slabs == 1); the slab layouts (has_xband 2-5) sum each column slab in
- * order and add the slab sums in slab order.  SM_ALGO_SELL keeps it for every row
+ * order and add the slab sums in slab order (band2 / cband after beta*y:
+ * sm_info.xband_beta_last).  SM_ALGO_SELL keeps it for every row
  * of up to 2048 terms and adds longer rows' 2048-term segment sums in order.  The
  * SpMM kernels keep it for every row.  SM_ALGO_STREAM keeps it for rows of up to
  * SM_SERIAL_ROW_MAX terms and uses a tree sum for longer rows.  The bound for

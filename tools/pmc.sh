@@ -5,7 +5,7 @@
 # (a 1 GiB float4 stream read of known size).  Output: gpurun_out/pmc/<name>/...
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$ROOT/gpurun_out/pmc
+OUT=${PMC_OUT:-$ROOT/gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
