@@ -423,18 +423,17 @@ static sm_status upload_band2(sm_matrix *m, const int32_t *rp, const int32_t *co
 
 // Gathered chunk bands (gcb.h, kernels_gcb.hip): 32K-row tiles where the rows make at
 // least 256 of them (one per CU), else 16K-row tiles; slabs so the tiles reach 256.
-static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
-    const int rows_log2 = m->n_rows >= ((int64_t)kXbTargetTiles << 15) ? 15 : 14;
+static void gcb_geometry(const sm_matrix *m, int &rows_log2, int32_t &slabs) {
+    rows_log2 = m->n_rows >= ((int64_t)kXbTargetTiles << 15) ? 15 : 14;
     const int64_t nblk = (m->n_rows + ((int64_t)1 << rows_log2) - 1) >> rows_log2;
-    int32_t slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
+    slabs = (int32_t)std::max<int64_t>(1, std::min<int64_t>(16, (kXbTargetTiles + nblk - 1) / nblk));
     if (m->opts.band_slabs > 0) slabs = m->opts.band_slabs;
-    GcbHost gh;
-    if (!gcb_build(rp, col, val, m->n_rows, m->n_cols, rows_log2, slabs, kGcbMaxWindow, gh)) return SM_OK;
+}
+
+// The rest of a built gcb layout (its bands already in d_chunk_start / d_band_clo / d_word):
+// slab partials, hand-off and pacing words, the geometry.
+static sm_status gcb_finish(sm_matrix *m, const GcbHost &gh) {
     XbandDev &d = m->plan.xb;
-    const int64_t ntile = (int64_t)gh.n_blocks * gh.n_slabs;
-    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, gh.n_bands), m->device_bytes));
-    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, gh.n_bands * kGcbBandWords), m->device_bytes));
     if (gh.n_slabs > 1) {
         const int64_t ps = (m->n_rows + 3) & ~(int64_t)3;   // 16-byte aligned partial rows
         SM_TRY_HIP(dev_alloc(&d.d_partials, (int64_t)(gh.n_slabs - 1) * ps, m->device_bytes));
@@ -446,13 +445,6 @@ static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col,
     d.pace_k = (int32_t)((m->n_cols + kGcbMaxWindow - 1) / kGcbMaxWindow);
     SM_TRY_HIP(dev_alloc(&d.d_pace, 8 * (1 + (int64_t)d.pace_k), m->device_bytes));
     SM_TRY_HIP(hipMemset(d.d_pace, 0, (size_t)8 * (1 + d.pace_k) * sizeof(int32_t)));
-    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, gh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
-                         hipMemcpyHostToDevice));
-    if (gh.n_bands > 0) {
-        SM_TRY_HIP(hipMemcpy(d.d_band_clo, gh.band_clo.data(), (size_t)gh.n_bands * 4, hipMemcpyHostToDevice));
-        SM_TRY_HIP(hipMemcpy(d.d_word, gh.ent.data(), (size_t)gh.n_bands * kGcbBandWords * 4,
-                             hipMemcpyHostToDevice));
-    }
     d.kind = kXbGcb;
     d.threads = 1024;
     d.block_rows = gh.block_rows;
@@ -464,6 +456,27 @@ static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col,
     d.max_chunks_per_band = gh.max_bands_per_tile;
     d.n_blocks = gh.n_blocks;
     return SM_OK;
+}
+
+static sm_status upload_gcb(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val) {
+    int rows_log2 = 0;
+    int32_t slabs = 1;
+    gcb_geometry(m, rows_log2, slabs);
+    GcbHost gh;
+    if (!gcb_build(rp, col, val, m->n_rows, m->n_cols, rows_log2, slabs, kGcbMaxWindow, gh)) return SM_OK;
+    XbandDev &d = m->plan.xb;
+    const int64_t ntile = (int64_t)gh.n_blocks * gh.n_slabs;
+    SM_TRY_HIP(dev_alloc(&d.d_chunk_start, ntile + 1, m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_band_clo, std::max<int64_t>(1, gh.n_bands), m->device_bytes));
+    SM_TRY_HIP(dev_alloc(&d.d_word, std::max<int64_t>(1, gh.n_bands * kGcbBandWords), m->device_bytes));
+    SM_TRY_HIP(hipMemcpy(d.d_chunk_start, gh.tile_band_start.data(), (size_t)(ntile + 1) * 4,
+                         hipMemcpyHostToDevice));
+    if (gh.n_bands > 0) {
+        SM_TRY_HIP(hipMemcpy(d.d_band_clo, gh.band_clo.data(), (size_t)gh.n_bands * 4, hipMemcpyHostToDevice));
+        SM_TRY_HIP(hipMemcpy(d.d_word, gh.ent.data(), (size_t)gh.n_bands * kGcbBandWords * 4,
+                             hipMemcpyHostToDevice));
+    }
+    return gcb_finish(m, gh);
 }
 
 sm_status upload_xband(sm_matrix *m, const int32_t *rp, const int32_t *col, const float *val,
@@ -1476,9 +1489,25 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
     // sort or exact sliced ELL, and no column-chunked ELL once the relabeling is decided (its
     // builder runs on the host).  R-MAT 24: the host path took 5.4 s.
     bool dev_done = false;
-    if (st == SM_OK && m->opts.host_build == 0 && !xband && !want_sweep(m.get()) && m->opts.hot_cols <= 0 &&
-        !want_merge_stage(m.get()) && m->opts.sell_sigma == 0 && m->opts.sell_streams <= 1 &&
-        m->opts.exact_sell != 1) {
+    const bool dev_ok = st == SM_OK && m->opts.host_build == 0 && !want_sweep(m.get()) && m->opts.hot_cols <= 0 &&
+                        !want_merge_stage(m.get()) && m->opts.sell_sigma == 0 && m->opts.sell_streams <= 1 &&
+                        m->opts.exact_sell != 1;
+    // The gathered chunk bands on the device (builddev_gcb.hip; config 5: 15 s on the host path).
+    // Declined (a row's columns not ascending, size limits): the host path below decides.
+    if (dev_ok && xband && xband_kind_setting(m.get()) == kXbGcb) {
+        hipError_t eb = hipSuccess;
+        int rows_log2 = 0;
+        int32_t slabs = 1;
+        gcb_geometry(m.get(), rows_log2, slabs);
+        GcbHost meta;
+        const int rc = devbuild_gcb(m.get(), rows_log2, slabs, kGcbMaxWindow, meta, s, eb);
+        if (rc < 0) st = hip_fail(eb, "device gcb builder");
+        else if (rc == 0) {
+            st = gcb_finish(m.get(), meta);
+            dev_done = st == SM_OK;
+        }
+    }
+    if (dev_ok && !xband) {
         hipError_t eb = hipSuccess;
         int rc = 0;
         if (want_relabel_size(m.get())) rc = devbuild_relabel(m.get(), m->opts.relabel != 1, s, eb);
@@ -1607,6 +1636,20 @@ sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]) {
         if ((st = fnv_dev(f, p.d_perm, p.n_relabel)) != SM_OK) return st;
         if ((st = fnv_dev(f, p.d_rcol, m->nnz)) != SM_OK) return st;
         digest[0] = f.h;
+    }
+    const XbandDev &xb = p.xb;
+    if (xb.kind == kXbGcb && xb.n_blocks > 0) {   // gathered chunk bands (gcb.h)
+        const int64_t ntile = (int64_t)xb.n_blocks * xb.n_slabs;
+        Fnv f;
+        const int32_t geo[5] = {xb.block_rows, xb.band_cols, xb.n_blocks, xb.n_slabs, xb.slab_bands};
+        f.add(geo, sizeof(geo));
+        if ((st = fnv_dev(f, xb.d_chunk_start, ntile + 1)) != SM_OK) return st;
+        if ((st = fnv_dev(f, xb.d_band_clo, xb.n_bands)) != SM_OK) return st;
+        digest[1] = f.h;
+        Fnv w;
+        if ((st = fnv_dev(w, xb.d_word, (int64_t)xb.n_bands * kGcbBandWords)) != SM_OK) return st;
+        digest[2] = w.h;
+        return SM_OK;
     }
     const SellDev &d = p.sell;
     if (d.n_slices > 0) {

@@ -306,6 +306,12 @@ int encode_csr_ref_device(const int32_t *d_rp, const int32_t *d_col, const float
 // upload_sell build on the host.  0 built or declined as the host would, -5 HIP error (err).
 int devbuild_relabel(sm_matrix *m, bool check_skew, hipStream_t s, hipError_t &err);
 int devbuild_sell(sm_matrix *m, int32_t max_len, bool codebook, hipStream_t s, hipError_t &err);
+// The gathered chunk bands (builddev_gcb.hip): gcb_build's bytes into m->plan.xb's d_chunk_start,
+// d_band_clo and d_word, the geometry in `meta` (its vectors stay empty).  0 built, 1 declined as
+// gcb_build would, < 0 on a HIP error (err) or a builder inconsistency.
+struct GcbHost;
+int devbuild_gcb(sm_matrix *m, int rows_log2, int32_t n_slabs, int32_t window, GcbHost &meta, hipStream_t s,
+                 hipError_t &err);
 hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
                            const int32_t *col, int32_t *d_flag, hipStream_t s);
 // Dense decode: out is zeroed by the caller.  b_layout: out[row*stride+col]

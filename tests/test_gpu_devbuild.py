@@ -117,3 +117,116 @@ def test_devbuild_config4_rmat24_full_size(sm):
     D, H, info = _both(sm, rp, ci, va, n)
     assert info["col_relabel"] == 1 and info["sell_codebook"] == 1, info
     _spmv_both(D, H, n, n, 8)
+
+
+# ---- gathered chunk bands (builddev_gcb.hip) -------------------------------------------------
+GKEYS = ("has_xband", "xband_slabs", "xband_slab_cols", "device_bytes", "sell_slices", "col_relabel")
+
+
+def _both_gcb(sm, rp, ci, va, n_cols, opts):
+    """Device and host builds of one CSR (device tensors): same layout bytes and info."""
+    torch = torch_dev()
+    dev = [a if hasattr(a, "device") else torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (rp, ci, va)]
+    out = []
+    for hb in (0, 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        M = sm.SparseMatrix.from_csr(*dev, n_cols, opts=dict(opts, host_build=hb))
+        torch.cuda.synchronize()
+        out.append((M, time.perf_counter() - t0))
+    (D, td), (H, th) = out
+    di, hi = D.info(), H.info()
+    assert {k: di[k] for k in GKEYS} == {k: hi[k] for k in GKEYS}, (di, hi)
+    assert D.layout_digest() == H.layout_digest(), (D.layout_digest(), H.layout_digest())
+    print(f"gcb build: device {td:.2f} s, host {th:.2f} s", {k: di[k] for k in GKEYS[:3]})
+    return D, H, di, td, th
+
+
+def _gcb_spmv_check(D, H, info, rp, ci, va, n_rows, n_cols, seed):
+    x = np.random.default_rng(seed).uniform(-1, 1, n_cols).astype(np.float32)
+    y0 = np.random.default_rng(seed + 1).uniform(-1, 1, n_rows).astype(np.float32)
+    torch = torch_dev()
+    yd, yh = torch.from_numpy(y0).cuda(), torch.from_numpy(y0).cuda()
+    xd = torch.from_numpy(x).cuda()
+    D.spmv(xd, yd, 1.3, 0.5)
+    H.spmv(xd, yh, 1.3, 0.5)
+    assert torch.equal(yd.view(torch.int32), yh.view(torch.int32))
+    if info["has_xband"] == 6 and info["xband_slabs"] == 1:   # one slab: the reference's order
+        want = oracle.csr_spmv(rp, ci, va, x, y0, 1.3, 0.5)
+        assert np.array_equal(bits(to_host(yd)), bits(want))
+
+
+@pytest.mark.parametrize("n_rows,n_cols,per_row", [(200003, 3000001, 16), (9000, 70001, 40), (5000, 1000, 5),
+                                                   (1, 50000, 30), (300000, 8000000, 4)])
+@pytest.mark.parametrize("slabs", [1, 0, 3])
+def test_devbuild_gcb_uniform(sm, n_rows, n_cols, per_row, slabs):
+    """Forced gcb on uniform shapes (test_gpu_gcb.py's), one, AUTO's and three slabs: the device
+    build's bands byte-identical to gcb.cpp's, the SpMV bit-identical (and with one slab the
+    reference's order)."""
+    from gpu_util import uniform_csr
+    rp, ci, va = uniform_csr(n_rows, n_cols, per_row, seed=n_rows + n_cols)
+    D, H, info, _, _ = _both_gcb(sm, rp, ci, va, n_cols, dict(layout="gcb", band_slabs=slabs))
+    assert info["has_xband"] == 6, info
+    _gcb_spmv_check(D, H, info, rp, ci, va, n_rows, n_cols, 3)
+
+
+def test_devbuild_gcb_long_segments_hub_columns(sm):
+    """Rows of 90 consecutive columns (cut inside the run: a band holds at most 63 terms of a
+    row), two hub columns in every row (a column's rows split over several bands)."""
+    rng = np.random.default_rng(3)
+    n_rows, n_cols, w = 6000, 700000, 90
+    rows = [np.union1d(np.arange(s, s + w), [5, 600000]) for s in rng.integers(0, n_cols - w - 10, n_rows)]
+    rp = np.zeros(n_rows + 1, np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    ci = np.concatenate(rows).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    for slabs in (1, 0):
+        D, H, info, _, _ = _both_gcb(sm, rp, ci, va, n_cols, dict(layout="gcb", band_slabs=slabs))
+        assert info["has_xband"] == 6, info
+        _gcb_spmv_check(D, H, info, rp, ci, va, n_rows, n_cols, 4)
+
+
+def test_devbuild_gcb_ragged_and_declines(sm):
+    """Empty rows, a 3000-term row, empty column ranges, a partial last block; and a row whose
+    columns are not ascending, which both builders decline (the same fallback layout)."""
+    rng = np.random.default_rng(11)
+    n_rows, n_cols = 40000, 2000000
+    lens = rng.integers(0, 12, n_rows)
+    lens[::50] = 0
+    lens[777] = 3000
+    rows = []
+    for r in range(n_rows):
+        lo, hi = (0, 300000) if r % 2 else (1200000, 2000000)
+        rows.append(np.sort(rng.choice(np.arange(lo, hi), int(lens[r]), replace=False)))
+    rp = np.zeros(n_rows + 1, np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    ci = np.concatenate(rows).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+    D, H, info, _, _ = _both_gcb(sm, rp, ci, va, n_cols, dict(layout="gcb", band_slabs=1))
+    assert info["has_xband"] == 6 and info["xband_slabs"] == 1, info
+    _gcb_spmv_check(D, H, info, rp, ci, va, n_rows, n_cols, 5)
+    ci2 = ci.copy()
+    a = int(rp[777])   # the 3000-term row: swap its first two columns
+    ci2[a], ci2[a + 1] = ci2[a + 1], ci2[a]
+    D2, H2, info2, _, _ = _both_gcb(sm, rp, ci2, va, n_cols, dict(layout="gcb", band_slabs=1))
+    assert info2["has_xband"] != 6, info2
+
+
+def test_devbuild_gcb_config5_rank0_slice(sm):
+    """Config 5's rank-0 slice as bench.py builds it (2^23 rows x 2^26 columns, 16 per row,
+    seed 5), AUTO: the device build byte-identical to the host's, under 1.5 s, the SpMV the
+    same bits."""
+    import sparsematrix_amd.synth as synth
+    n_rows, n_cols = 1 << 23, 1 << 26
+    rp, ci, va = synth.uniform_rows_device(n_rows, n_cols, 16, seed=5)
+    D, H, info, td, th = _both_gcb(sm, rp, ci, va, n_cols, {})
+    assert info["has_xband"] == 6, info
+    torch = torch_dev()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.rand(n_cols, device="cuda", generator=g) * 2 - 1
+    y0 = torch.rand(n_rows, device="cuda", generator=g) * 2 - 1
+    yd, yh = y0.clone(), y0.clone()
+    D.spmv(x, yd, 1.0, 0.5)
+    H.spmv(x, yh, 1.0, 0.5)
+    assert torch.equal(yd.view(torch.int32), yh.view(torch.int32))
+    assert td < 1.5, (td, th)
