@@ -267,10 +267,14 @@ def main():
         raise SystemExit("the columns must split evenly over the ranks (one all-gather)")
 
     t_build0 = time.perf_counter()
+    gen_s = 0.0
     reps = []
     for k in range(replicas):
         seed = seed0 + 1000 * k + 7919 * rank
+        t_g0 = time.perf_counter()
         rp, ci, va = synth.uniform_rows_device(R, C, per, seed=seed, device=dev)
+        torch.cuda.synchronize()
+        gen_s += time.perf_counter() - t_g0
         bopts = {} if args.layout == "auto" else dict(layout=args.layout)
         if args.band_tall:
             bopts["band_tall"] = args.band_tall
@@ -645,6 +649,8 @@ def main():
                        "alpha": 1.0, "beta": 0.5, "launch": "hip_graph" if use_graph else "eager",
                        "build_s": round(build_s, 1),   # every replica: generation + layout build
                        "build_s_per_matrix": round(build_s / max(replicas, 1), 2),
+                       "generate_s": round(gen_s, 2),   # of which the synthetic CSR generation
+                       "layout_build_s_per_matrix": round((build_s - gen_s) / max(replicas, 1), 2),
                        "parallelism": f"row-partition x{world}" + (
                            f", {path}" + (": all-gather of step k+1 beside SpMV k"
                                           if overlap else "") if world > 1 else ""),
@@ -722,6 +728,8 @@ def config5_line(args, torch, dist, world, rank, dev, dev_index, rehearse) -> di
     R = C // world
     t_b = time.perf_counter()
     rp, ci, va = synth.uniform_rows_device(R, C, per, seed=5 + 7919 * rank, device=dev)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t_b
     M = smd.SparseMatrix.from_csr(rp, ci, va, C, device=dev_index,
                                   opts=None if args.layout == "auto" else dict(layout=args.layout))
     del rp, ci, va
@@ -782,7 +790,8 @@ def config5_line(args, torch, dist, world, rank, dev, dev_index, rehearse) -> di
            "alg_bytes_total": bytes_total, "alg_bytes_rank": bytes_rank,
            "local_spmv_ms_max_over_ranks": round(lms, 4), "local_spmv_ms_rank0": stats(local),
            "kernel_frac": round(bytes_rank / (lms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-           "layout": lay, "kernel": KERNELS.get(lay, lay), "build_s": round(build_s, 1),
+           "layout": lay, "kernel": KERNELS.get(lay, lay), "build_s": round(build_s, 1), "generate_s": round(gen_s, 2),
+           "layout_build_s": round(build_s - gen_s, 2),
            "traffic": traffic,
            "traffic_source": (f"profiles/traffic_{wl}_{lay}.json (rocprofv3 PMC)" if traffic else None),
            "path": ("one SpMV of the whole matrix per step" if ctx is None else
