@@ -27,7 +27,9 @@
 // exactly the reference's order after beta (kernel.cc:10-29, sparse-matrix.cc:149-151).
 #include "sm_internal.h"
 
+#include <algorithm>
 #include <cstdio>
+#include <vector>
 
 namespace smamd {
 namespace {
@@ -421,6 +423,168 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     }
 }
 
+// The same lists by a stable counting sort instead of the bitmap (round 6): the bitmap
+// kernel's 53 KB of LDS (bitmap + word prefixes) allowed ~2 resident workgroups per CU, so the
+// 1164 (batch, group) workgroups of a sparse 16K x 16K stream ran in ~2.3 generations of one
+// dependent chain each.  Here a workgroup needs 22 KB and no bitmap clearing:
+//   decode   as above (thread t: entries 16 t .. 16 t + 15, one 16-byte load each of deltas
+//            and ids); every entry's word (row | id << 23) and column in the group (0xFF: dead)
+//            go to LDS in stream order;
+//   rank     wave w takes entries 1024 w .. 1024 w + 1023, 64 consecutive per step (lane =
+//            entry): six ballots of the column bits give each lane the lanes of its column,
+//            its rank among them, and a per-wave running count per column (one writer per
+//            column and step) adds the earlier steps -- a stable rank in stream order; m = 1
+//            issues the x gathers here, consumed after two barriers;
+//   offsets  wave 0 sums each column's four wave counts and scans over the 64 columns: the
+//            list header, and per (wave, column) the start of its run;
+//   place    each live entry's value at start + rank, staged in LDS over the words, stored
+//            coalesced.
+// Lists, headers and values are the bitmap kernel's, bit for bit.
+// TS (development builds, SM_NAT_TS): thread 0 stamps s_memrealtime (100 MHz) at the start,
+// after the stream load, after the rank steps and at the end into ts[4 * workgroup + k].
+[[maybe_unused]] __device__ __forceinline__ unsigned long long nat_rt() {
+    unsigned long long v;
+    asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(v));
+    return v;
+}
+
+template <bool X1, bool TS = false>
+__global__ __launch_bounds__(kNatThreads) void native_decode_sort_kernel(
+    const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
+    const NatBatch *__restrict__ bmeta, const int32_t *__restrict__ boff,
+    const float *__restrict__ table, int32_t T, const float *__restrict__ x, float alpha,
+    uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr, unsigned long long *__restrict__ ts = nullptr) {
+    constexpr int kWaves = kNatThreads / 64;
+    const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if constexpr (TS) {
+        if (threadIdx.x == 0) ts[4 * wg] = nat_rt();
+    }
+    __shared__ float tab[X1 ? 256 : 1];
+    __shared__ uint32_t lw[kNatBatch];               // row | id << 23, then the staged values
+    __shared__ uint8_t lc[kNatBatch];                // column in the group, 0xFF: dead
+    __shared__ int32_t wcnt[kWaves][kNatCols];       // running counts, then run starts
+    __shared__ int32_t wsum[kWaves];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int32_t b = blockIdx.x, g = blockIdx.y;
+    const NatBatch bm = bmeta[b];
+    const int64_t e0 = bm.start, e_end = bm.start + bm.len;
+    const int32_t list_off = boff[b * 4 + g];
+    if (X1) tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
+    if (t < kNatCols) {
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) wcnt[w][t] = 0;
+    }
+    uint8_t d[kNatPer], id[kNatPer];
+    {
+        const int64_t e = e0 + (int64_t)t * kNatPer;
+        if (e + kNatPer <= e_end) {   // 16-byte aligned (upload_native)
+            const uint4 dv = *reinterpret_cast<const uint4 *>(pos + e);
+            const uint4 iv = *reinterpret_cast<const uint4 *>(val + e);
+            __builtin_memcpy(d, &dv, 16);
+            __builtin_memcpy(id, &iv, 16);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kNatPer; ++k) {
+                const bool in = e + k < e_end;
+                d[k] = in ? pos[e + k] : 0;
+                id[k] = in ? val[e + k] : 255;
+            }
+        }
+    }
+    int32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kNatPer; ++k) tot += d[k];
+    if constexpr (TS) {
+        if (threadIdx.x == 0) ts[4 * wg + 1] = nat_rt() + (unsigned long long)(tot & 0);
+    }
+    const int32_t incl = wave_incl_scan(tot, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int32_t off = bm.carry + incl - tot;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w)
+        if (w < wave) off += wsum[w];
+    {
+        uint32_t wv[kNatPer];
+        uint8_t cv[kNatPer];
+#pragma unroll
+        for (int k = 0; k < kNatPer; ++k) {
+            off += d[k];
+            const int32_t pc = off & 255;
+            const bool live = id[k] < T && (pc >> 6) == g;
+            wv[k] = (uint32_t)(off >> 8) | ((uint32_t)id[k] << 23);
+            cv[k] = live ? (uint8_t)(pc & 63) : (uint8_t)0xFF;
+        }
+        uint4 *lw4 = reinterpret_cast<uint4 *>(lw + t * kNatPer);
+#pragma unroll
+        for (int q = 0; q < kNatPer / 4; ++q)
+            lw4[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+        uint4 c4;
+        __builtin_memcpy(&c4, cv, 16);
+        *reinterpret_cast<uint4 *>(lc + t * kNatPer) = c4;
+    }
+    __syncthreads();
+    // rank: per step, entry 1024 wave + 64 s + lane
+    int32_t rc[kNatPer];   // live: column << 24 | id << 16 | rank in the wave's run; dead: -1
+    uint32_t wr[kNatPer];  // X1: x bits; else the word
+#pragma unroll
+    for (int s = 0; s < kNatPer; ++s) {
+        const int e = 1024 * wave + 64 * s + lane;
+        const int32_t c = lc[e];
+        const uint32_t w = lw[e];
+        const bool live = c < kNatCols;
+        if constexpr (X1) wr[s] = live ? __float_as_uint(x[w & 0x7FFFFFu]) : 0u;
+        else wr[s] = w;
+        uint64_t same = __ballot(live);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+            const uint64_t mb = __ballot((c >> bb) & 1);
+            same &= ((c >> bb) & 1) ? mb : ~mb;
+        }
+        const int32_t cl = c & (kNatCols - 1);
+        const int32_t base = wcnt[wave][cl];
+        const int32_t rank = base + (int32_t)__popcll(same & ((1ull << lane) - 1ull));
+        rc[s] = live ? (cl << 24) | ((int32_t)(w >> 23) << 16) | rank : -1;
+        if (live && (same >> lane) == 1ull) wcnt[wave][cl] = base + (int32_t)__popcll(same);
+    }
+    __syncthreads();
+    if constexpr (TS) {
+        if (threadIdx.x == 0) ts[4 * wg + 2] = nat_rt();
+    }
+    if (wave == 0) {   // lane = column: the header, the runs' starts, the group's live count
+        int32_t cn[kWaves], ctot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            cn[w] = wcnt[w][lane];
+            ctot += cn[w];
+        }
+        const int32_t cincl = wave_incl_scan(ctot, lane);
+        int32_t cb = cincl - ctot;
+        hdr[((int64_t)b * 4 + g) * kNatCols + lane] = (uint32_t)cb | ((uint32_t)cincl << 16);
+        if (lane == 63) wsum[0] = cincl;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            wcnt[w][lane] = cb;
+            cb += cn[w];
+        }
+    }
+    __syncthreads();
+    const int32_t n_live = wsum[0];
+#pragma unroll
+    for (int s = 0; s < kNatPer; ++s) {
+        if (rc[s] < 0) continue;
+        const int32_t cl = rc[s] >> 24, idv = (rc[s] >> 16) & 255, rank = rc[s] & 0xFFFF;
+        lw[wcnt[wave][cl] + rank] = X1 ? __float_as_uint(__fmul_rn(__uint_as_float(wr[s]), tab[idv])) : wr[s];
+    }
+    __syncthreads();
+    uint32_t *out = lists + list_off;
+    for (int32_t i = t; i < n_live; i += kNatThreads) out[i] = lw[i];
+    if constexpr (TS) {
+        __syncthreads();
+        if (threadIdx.x == 0) ts[4 * wg + 3] = nat_rt();
+    }
+}
+
 // One thread per (column, RT rows of A); X1: one wave per (panel, group), the terms added.
 template <int RT, bool X1>
 __global__ __launch_bounds__(X1 ? 64 : kNatThreads) void native_apply_kernel(
@@ -726,17 +890,60 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
         const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;
         if (nd.n_batches > 0) {
             const dim3 dgrid((unsigned)nd.n_batches, 256 / kNatCols);
-            if (m == 1)
+            bool bitmap = false;   // the bitmap decode (rounds 3-5), kept for A/B
+#ifdef SM_DEV
+            if (const char *e = dev_env("SM_NAT_BITMAP")) bitmap = atoi(e) != 0;
+#endif
+            if (bitmap && m == 1)
                 hipLaunchKernelGGL(native_decode_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
                                    nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
                                    nd.d_lists, nd.d_hdr);
-            else
+            else if (bitmap)
                 hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                   nd.d_lists, nd.d_hdr);
+            else if (m == 1)
+                hipLaunchKernelGGL(native_decode_sort_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                   nd.d_lists, nd.d_hdr);
+            else
+                hipLaunchKernelGGL(native_decode_sort_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
                                    nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
                                    nd.d_lists, nd.d_hdr);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
 #ifdef SM_DEV
+            if (m == 1 && !bitmap && dev_env("SM_NAT_TS")) {   // the decode again, stamped (same outputs)
+                const int64_t nw = (int64_t)nd.n_batches * 4;
+                unsigned long long *d = nullptr;
+                std::vector<unsigned long long> h((size_t)nw * 4);
+                if (hipMalloc(&d, h.size() * 8) != hipSuccess) return hipErrorOutOfMemory;
+                hipLaunchKernelGGL((native_decode_sort_kernel<true, true>), dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
+                                   nd.d_lists, nd.d_hdr, d);
+                (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                (void)hipFree(d);
+                unsigned long long t0 = ~0ull, t1 = 0;
+                for (int64_t i = 0; i < nw; i++) t0 = std::min(t0, h[(size_t)(4 * i)]), t1 = std::max(t1, h[(size_t)(4 * i + 3)]);
+                std::vector<double> st, life, load, rank, tail;
+                for (int64_t i = 0; i < nw; i++) {
+                    const unsigned long long *q = &h[(size_t)(4 * i)];
+                    st.push_back((q[0] - t0) / 100.0);
+                    life.push_back((q[3] - q[0]) / 100.0);
+                    load.push_back((q[1] - q[0]) / 100.0);
+                    rank.push_back((q[2] - q[1]) / 100.0);
+                    tail.push_back((q[3] - q[2]) / 100.0);
+                }
+                auto pct = [](std::vector<double> v, double f) {
+                    std::sort(v.begin(), v.end());
+                    return v[(size_t)std::min<double>((double)v.size() - 1, f * (double)v.size())];
+                };
+                fprintf(stderr, "native decode ts (us, %lld wgs): span %.2f | start p50 %.2f p90 %.2f max %.2f | life p50 %.2f p90 %.2f max %.2f | "
+                        "load p50 %.2f p90 %.2f | rank p50 %.2f p90 %.2f | tail p50 %.2f p90 %.2f\n", (long long)nw,
+                        (t1 - t0) / 100.0, pct(st, .5), pct(st, .9), pct(st, 1), pct(life, .5), pct(life, .9), pct(life, 1),
+                        pct(load, .5), pct(load, .9), pct(rank, .5), pct(rank, .9), pct(tail, .5), pct(tail, .9));
+            }
             if (dev_env("SM_NAT_PROF")) {   // the decode again, profiled (same outputs)
                 unsigned long long *d = nullptr, h[8] = {};
                 if (hipMalloc(&d, sizeof(h)) != hipSuccess) return hipErrorOutOfMemory;
