@@ -423,23 +423,6 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     }
 }
 
-// The same lists by a stable counting sort instead of the bitmap (round 6): the bitmap
-// kernel's 53 KB of LDS (bitmap + word prefixes) allowed ~2 resident workgroups per CU, so the
-// 1164 (batch, group) workgroups of a sparse 16K x 16K stream ran in ~2.3 generations of one
-// dependent chain each.  Here a workgroup needs 22 KB and no bitmap clearing:
-//   decode   as above (thread t: entries 16 t .. 16 t + 15, one 16-byte load each of deltas
-//            and ids); every entry's word (row | id << 23) and column in the group (0xFF: dead)
-//            go to LDS in stream order;
-//   rank     wave w takes entries 1024 w .. 1024 w + 1023, 64 consecutive per step (lane =
-//            entry): six ballots of the column bits give each lane the lanes of its column,
-//            its rank among them, and a per-wave running count per column (one writer per
-//            column and step) adds the earlier steps -- a stable rank in stream order; m = 1
-//            issues the x gathers here, consumed after two barriers;
-//   offsets  wave 0 sums each column's four wave counts and scans over the 64 columns: the
-//            list header, and per (wave, column) the start of its run;
-//   place    each live entry's value at start + rank, staged in LDS over the words, stored
-//            coalesced.
-// Lists, headers and values are the bitmap kernel's, bit for bit.
 // TS (development builds, SM_NAT_TS): thread 0 stamps s_memrealtime (100 MHz) at the start,
 // after the stream load, after the rank steps and at the end into ts[4 * workgroup + k].
 [[maybe_unused]] __device__ __forceinline__ unsigned long long nat_rt() {
@@ -448,54 +431,67 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_kernel(
     return v;
 }
 
+// The same lists by a stable counting sort, one 1024-thread workgroup per batch for all four
+// column groups (round 6; the default).  The bitmap kernel above decodes every batch four times
+// (once per group) and its 53 KB of LDS allow ~2 workgroups per CU.  A per-(batch, group)
+// counting sort with 22 KB (one generation, all workgroups resident from the start) still took
+// 10.7 us per workgroup by per-workgroup stamps (SM_NAT_TS): VALU issue -- ≈ 2000 instructions
+// per wave, 5 waves per SIMD, 4 cycles per wave64 instruction -- not latency, bounded it.  Here
+// each entry is decoded and ranked once:
+//   decode   thread t: entries 4 t .. 4 t + 3 (one 4-byte load each of deltas and ids), a wave
+//            scan and the 16 wave totals give the offsets; word (row | id << 23) and column
+//            (0x100: dead) to LDS in stream order;
+//   rank     wave w: entries 256 w .. 256 w + 255, 64 consecutive per step, eight ballots of
+//            the column bits, a per-wave running count per column (as above);
+//   offsets  waves 0-3 take columns 64 g .. 64 g + 63 (group g): each column's 16 wave counts,
+//            a wave scan (the group's header) and the group totals;
+//   place    staged in LDS and stored coalesced: the batch's groups are contiguous in the
+//            lists (upload_native: boff[4 b + g] = boff[4 b] + the live entries of groups < g).
 template <bool X1, bool TS = false>
-__global__ __launch_bounds__(kNatThreads) void native_decode_sort_kernel(
+__global__ __launch_bounds__(1024) void native_decode_batch_kernel(
     const uint8_t *__restrict__ pos, const uint8_t *__restrict__ val,
     const NatBatch *__restrict__ bmeta, const int32_t *__restrict__ boff,
     const float *__restrict__ table, int32_t T, const float *__restrict__ x, float alpha,
     uint32_t *__restrict__ lists, uint32_t *__restrict__ hdr, unsigned long long *__restrict__ ts = nullptr) {
-    constexpr int kWaves = kNatThreads / 64;
-    const int64_t wg = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-    if constexpr (TS) {
-        if (threadIdx.x == 0) ts[4 * wg] = nat_rt();
-    }
+    constexpr int kThr = 1024, kWaves = kThr / 64, kPer = kNatBatch / kThr;   // 4 entries per thread
+    static_assert(kPer == 4, "one 4-byte load of deltas and ids per thread");
     __shared__ float tab[X1 ? 256 : 1];
     __shared__ uint32_t lw[kNatBatch];               // row | id << 23, then the staged values
-    __shared__ uint8_t lc[kNatBatch];                // column in the group, 0xFF: dead
-    __shared__ int32_t wcnt[kWaves][kNatCols];       // running counts, then run starts
+    __shared__ uint16_t lc[kNatBatch];               // column, 0x100: dead
+    __shared__ int32_t wcnt[kWaves][256];            // running counts, then run starts
     __shared__ int32_t wsum[kWaves];
+    __shared__ int32_t gtot[4];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int32_t b = blockIdx.x, g = blockIdx.y;
+    const int32_t b = blockIdx.x;
+    if constexpr (TS) {
+        if (t == 0) ts[4 * b] = nat_rt();
+    }
     const NatBatch bm = bmeta[b];
     const int64_t e0 = bm.start, e_end = bm.start + bm.len;
-    const int32_t list_off = boff[b * 4 + g];
-    if (X1) tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
-    if (t < kNatCols) {
+    const int32_t list_off = boff[b * 4];
+    if (X1 && t < 256) tab[t] = t < T ? __fmul_rn(table[t], alpha) : 0.0f;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) wcnt[w][t] = 0;
-    }
-    uint8_t d[kNatPer], id[kNatPer];
+    for (int k = 0; k < kWaves * 256 / kThr; ++k) (&wcnt[0][0])[t + k * kThr] = 0;
+    uint8_t d[kPer], id[kPer];
     {
-        const int64_t e = e0 + (int64_t)t * kNatPer;
-        if (e + kNatPer <= e_end) {   // 16-byte aligned (upload_native)
-            const uint4 dv = *reinterpret_cast<const uint4 *>(pos + e);
-            const uint4 iv = *reinterpret_cast<const uint4 *>(val + e);
-            __builtin_memcpy(d, &dv, 16);
-            __builtin_memcpy(id, &iv, 16);
+        const int64_t e = e0 + (int64_t)t * kPer;
+        if (e + kPer <= e_end) {   // batch starts are 16-byte aligned (upload_native)
+            const uint32_t dv = *reinterpret_cast<const uint32_t *>(pos + e);
+            const uint32_t iv = *reinterpret_cast<const uint32_t *>(val + e);
+            __builtin_memcpy(d, &dv, 4);
+            __builtin_memcpy(id, &iv, 4);
         } else {
 #pragma unroll
-            for (int k = 0; k < kNatPer; ++k) {
+            for (int k = 0; k < kPer; ++k) {
                 const bool in = e + k < e_end;
                 d[k] = in ? pos[e + k] : 0;
                 id[k] = in ? val[e + k] : 255;
             }
         }
     }
-    int32_t tot = 0;
-#pragma unroll
-    for (int k = 0; k < kNatPer; ++k) tot += d[k];
+    const int32_t tot = (int32_t)d[0] + d[1] + d[2] + d[3];
     if constexpr (TS) {
-        if (threadIdx.x == 0) ts[4 * wg + 1] = nat_rt() + (unsigned long long)(tot & 0);
+        if (t == 0) ts[4 * b + 1] = nat_rt() + (unsigned long long)(tot & 0);
     }
     const int32_t incl = wave_incl_scan(tot, lane);
     if (lane == 63) wsum[wave] = incl;
@@ -505,83 +501,84 @@ __global__ __launch_bounds__(kNatThreads) void native_decode_sort_kernel(
     for (int w = 0; w < kWaves; ++w)
         if (w < wave) off += wsum[w];
     {
-        uint32_t wv[kNatPer];
-        uint8_t cv[kNatPer];
+        uint32_t wv[kPer];
+        uint16_t cv[kPer];
 #pragma unroll
-        for (int k = 0; k < kNatPer; ++k) {
+        for (int k = 0; k < kPer; ++k) {
             off += d[k];
-            const int32_t pc = off & 255;
-            const bool live = id[k] < T && (pc >> 6) == g;
             wv[k] = (uint32_t)(off >> 8) | ((uint32_t)id[k] << 23);
-            cv[k] = live ? (uint8_t)(pc & 63) : (uint8_t)0xFF;
+            cv[k] = id[k] < T ? (uint16_t)(off & 255) : (uint16_t)0x100;
         }
-        uint4 *lw4 = reinterpret_cast<uint4 *>(lw + t * kNatPer);
-#pragma unroll
-        for (int q = 0; q < kNatPer / 4; ++q)
-            lw4[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
-        uint4 c4;
-        __builtin_memcpy(&c4, cv, 16);
-        *reinterpret_cast<uint4 *>(lc + t * kNatPer) = c4;
+        *reinterpret_cast<uint4 *>(lw + t * kPer) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        uint2 c2;
+        __builtin_memcpy(&c2, cv, 8);
+        *reinterpret_cast<uint2 *>(lc + t * kPer) = c2;
     }
     __syncthreads();
-    // rank: per step, entry 1024 wave + 64 s + lane
-    int32_t rc[kNatPer];   // live: column << 24 | id << 16 | rank in the wave's run; dead: -1
-    uint32_t wr[kNatPer];  // X1: x bits; else the word
+    uint32_t rc[kPer];   // live: column << 24 | id << 16 | rank in the wave's run; dead: ~0
+    uint32_t wr[kPer];   // X1: x bits; else the word
 #pragma unroll
-    for (int s = 0; s < kNatPer; ++s) {
-        const int e = 1024 * wave + 64 * s + lane;
+    for (int s = 0; s < kPer; ++s) {
+        const int e = 256 * wave + 64 * s + lane;
         const int32_t c = lc[e];
         const uint32_t w = lw[e];
-        const bool live = c < kNatCols;
+        const bool live = c < 256;
         if constexpr (X1) wr[s] = live ? __float_as_uint(x[w & 0x7FFFFFu]) : 0u;
         else wr[s] = w;
         uint64_t same = __ballot(live);
 #pragma unroll
-        for (int bb = 0; bb < 6; ++bb) {
+        for (int bb = 0; bb < 8; ++bb) {
             const uint64_t mb = __ballot((c >> bb) & 1);
             same &= ((c >> bb) & 1) ? mb : ~mb;
         }
-        const int32_t cl = c & (kNatCols - 1);
+        const int32_t cl = c & 255;
         const int32_t base = wcnt[wave][cl];
-        const int32_t rank = base + (int32_t)__popcll(same & ((1ull << lane) - 1ull));
-        rc[s] = live ? (cl << 24) | ((int32_t)(w >> 23) << 16) | rank : -1;
+        const uint32_t rank = (uint32_t)base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        rc[s] = live ? ((uint32_t)cl << 24) | ((w >> 23) << 16) | rank : ~0u;
         if (live && (same >> lane) == 1ull) wcnt[wave][cl] = base + (int32_t)__popcll(same);
     }
     __syncthreads();
     if constexpr (TS) {
-        if (threadIdx.x == 0) ts[4 * wg + 2] = nat_rt();
+        if (t == 0) ts[4 * b + 2] = nat_rt();
     }
-    if (wave == 0) {   // lane = column: the header, the runs' starts, the group's live count
-        int32_t cn[kWaves], ctot = 0;
+    int32_t cn[kWaves], ctot = 0, cincl = 0;
+    if (wave < 4) {   // column 64 wave + lane of group `wave`
+        const int c = t;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) {
-            cn[w] = wcnt[w][lane];
+            cn[w] = wcnt[w][c];
             ctot += cn[w];
         }
-        const int32_t cincl = wave_incl_scan(ctot, lane);
+        cincl = wave_incl_scan(ctot, lane);
+        hdr[((int64_t)b * 4 + wave) * kNatCols + lane] = (uint32_t)(cincl - ctot) | ((uint32_t)cincl << 16);
+        if (lane == 63) gtot[wave] = cincl;
+    }
+    __syncthreads();
+    const int32_t n_live = gtot[0] + gtot[1] + gtot[2] + gtot[3];
+    if (wave < 4) {
         int32_t cb = cincl - ctot;
-        hdr[((int64_t)b * 4 + g) * kNatCols + lane] = (uint32_t)cb | ((uint32_t)cincl << 16);
-        if (lane == 63) wsum[0] = cincl;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            if (g < wave) cb += gtot[g];
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) {
-            wcnt[w][lane] = cb;
+            wcnt[w][t] = cb;
             cb += cn[w];
         }
     }
     __syncthreads();
-    const int32_t n_live = wsum[0];
 #pragma unroll
-    for (int s = 0; s < kNatPer; ++s) {
-        if (rc[s] < 0) continue;
-        const int32_t cl = rc[s] >> 24, idv = (rc[s] >> 16) & 255, rank = rc[s] & 0xFFFF;
+    for (int s = 0; s < kPer; ++s) {
+        if (rc[s] == ~0u) continue;
+        const int32_t cl = (int32_t)(rc[s] >> 24), idv = (int32_t)((rc[s] >> 16) & 255), rank = (int32_t)(rc[s] & 0xFFFF);
         lw[wcnt[wave][cl] + rank] = X1 ? __float_as_uint(__fmul_rn(__uint_as_float(wr[s]), tab[idv])) : wr[s];
     }
     __syncthreads();
     uint32_t *out = lists + list_off;
-    for (int32_t i = t; i < n_live; i += kNatThreads) out[i] = lw[i];
+    for (int32_t i = t; i < n_live; i += kThr) out[i] = lw[i];
     if constexpr (TS) {
         __syncthreads();
-        if (threadIdx.x == 0) ts[4 * wg + 3] = nat_rt();
+        if (t == 0) ts[4 * b + 3] = nat_rt();
     }
 }
 
@@ -886,41 +883,44 @@ hipError_t launch_native_addmatmat(const NativeDev &nd, int32_t m, const float *
         return hipGetLastError();
     }
     if (nd.max_panel_batches > kNatFusedBatches && nd.d_lists) {
-        // Two kernels: decode every (batch, group) at once, then walk the lists.
+        // Two kernels: decode every batch at once, then walk the lists.
         const int RT = m == 1 ? 1 : m <= 4 ? 1 : m <= 8 ? 2 : m <= 16 ? 4 : 8;
         if (nd.n_batches > 0) {
             const dim3 dgrid((unsigned)nd.n_batches, 256 / kNatCols);
-            bool bitmap = false;   // the bitmap decode (rounds 3-5), kept for A/B
+            // One workgroup per batch (native_decode_batch_kernel); development builds keep the
+            // per-(batch, group) bitmap form of rounds 3-5 for A/B (SM_NAT_DECODE=0).
+            bool bitmap = false;
 #ifdef SM_DEV
-            if (const char *e = dev_env("SM_NAT_BITMAP")) bitmap = atoi(e) != 0;
+            if (const char *e = dev_env("SM_NAT_DECODE")) bitmap = atoi(e) == 0;
 #endif
-            if (bitmap && m == 1)
+            if (!bitmap) {
+                if (m == 1)
+                    hipLaunchKernelGGL(native_decode_batch_kernel<true>, dim3((unsigned)nd.n_batches), dim3(1024), 0, s,
+                                       nd.d_pos, nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a,
+                                       alpha, nd.d_lists, nd.d_hdr);
+                else
+                    hipLaunchKernelGGL(native_decode_batch_kernel<false>, dim3((unsigned)nd.n_batches), dim3(1024), 0, s,
+                                       nd.d_pos, nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a,
+                                       alpha, nd.d_lists, nd.d_hdr);
+            } else if (m == 1)
                 hipLaunchKernelGGL(native_decode_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
                                    nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
                                    nd.d_lists, nd.d_hdr);
-            else if (bitmap)
-                hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
-                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
-                                   nd.d_lists, nd.d_hdr);
-            else if (m == 1)
-                hipLaunchKernelGGL(native_decode_sort_kernel<true>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
-                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
-                                   nd.d_lists, nd.d_hdr);
             else
-                hipLaunchKernelGGL(native_decode_sort_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
+                hipLaunchKernelGGL(native_decode_kernel<false>, dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
                                    nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
                                    nd.d_lists, nd.d_hdr);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
 #ifdef SM_DEV
             if (m == 1 && !bitmap && dev_env("SM_NAT_TS")) {   // the decode again, stamped (same outputs)
-                const int64_t nw = (int64_t)nd.n_batches * 4;
+                const int64_t nw = (int64_t)nd.n_batches;
                 unsigned long long *d = nullptr;
                 std::vector<unsigned long long> h((size_t)nw * 4);
                 if (hipMalloc(&d, h.size() * 8) != hipSuccess) return hipErrorOutOfMemory;
-                hipLaunchKernelGGL((native_decode_sort_kernel<true, true>), dgrid, dim3(kNatThreads), 0, s, nd.d_pos,
-                                   nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a, alpha,
-                                   nd.d_lists, nd.d_hdr, d);
+                hipLaunchKernelGGL((native_decode_batch_kernel<true, true>), dim3((unsigned)nd.n_batches), dim3(1024), 0,
+                                   s, nd.d_pos, nd.d_val, nd.d_bmeta, nd.d_boff, nd.d_table, nd.table_size, a,
+                                   alpha, nd.d_lists, nd.d_hdr, d);
                 (void)hipMemcpyAsync(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost, s);
                 (void)hipStreamSynchronize(s);
                 (void)hipFree(d);
