@@ -306,9 +306,18 @@ static bool gather_cost_ok(const sm_matrix *m) {
     return gather_us < sell_us;
 }
 
+// Below this many terms AUTO keeps the sorted sliced ELL instead of a swept band layout: a
+// band SpMV carries ~20 us of fixed cost (x staging per tile, the slab hand-off) that small
+// matrices do not amortise, and their few row blocks leave CUs idle (16K rows: 16 tiles).
+// Uniform 16-per-row squares, eager SpMV incl. launch (tools/small_auto_ab.py,
+// profiles/r06_small_auto_ab.txt): 2^18 rows (4.2 M terms) cband 31.3 vs sell 22.3 us,
+// 2^19 (8.4 M) 34.6 vs 41.6 us.
+constexpr int64_t kBandMinNnz = 6 * ((int64_t)1 << 20);
+
 static bool xband_cost_ok(const sm_matrix *m, XbKind kind) {
     if ((kind == kXbGather || kind == kXbGcb) && m->n_cols > kGatherCols && m->opts.gather_band_log2 == 0)
         return gather_cost_ok(m);   // gcb: ~2x faster than the gather kind it is priced as
+    if (m->nnz < kBandMinNnz) return false;
     const int rows_log2 = kind == kXbExact    ? kXbExactRowsLog2
                           : kind == kXbBand2 || kind == kXbCband ? kB2RowBits
                           : kind == kXbGather ? kXbGatherRowsLog2

@@ -410,7 +410,7 @@ def test_concurrent_spmvs_on_two_streams(sm):
     torch = torch_dev()
     n_rows, n_cols = 300000, 400000
     rp, ci, va = uniform_csr(n_rows, n_cols, 16, seed=31)
-    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols)
+    M = sm.SparseMatrix.from_csr(rp, ci, va, n_cols, opts=dict(layout="bands"))   # AUTO: < 6 M terms, sell
     info = M.info()
     assert info["has_xband"] == 5 and info["xband_slabs"] > 1, info
     rng = np.random.default_rng(32)
