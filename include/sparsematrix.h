@@ -294,7 +294,8 @@ SM_API sm_status sm_get_info_ex(const sm_matrix *m, sm_info *info, size_t info_b
  * compared byte for byte (sm_build_opts.host_build): [0] the column relabeling (new column
  * of every original column, relabeled col_idx), [1] the sorted sliced ELL's structure
  * (slice offsets and lengths, lane rows and lengths, long rows and their partial offsets),
- * [2] its slots (column words, values), [3] its codebook.  0 for a part not built.  With the
+ * [2] its slots (column words, values), [3] its codebook and the merge path's staging copy
+ * (sm_build_opts.merge_stage: column words, offsets, table).  0 for a part not built.  With the
  * gathered chunk bands (SM_LAYOUT_GCB) [1] is their geometry, tile -> band offsets and band
  * start columns, [2] the bands' words.  Synchronises the device. */
 SM_API sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]);

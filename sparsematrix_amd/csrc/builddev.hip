@@ -12,13 +12,17 @@
 //   sell      units (rows of <= max_len terms, max_len-term segments of longer rows, in row
 //             order), a stable radix sort by descending length, 64 units per slice, slice
 //             lengths rounded up to kSellUnroll, offsets by an exclusive scan, and one wave per
-//             slice writing its lanes' terms column-interleaved (zero padding).
+//             slice writing its lanes' terms column-interleaved (zero padding);
+//   merge     the merge path's column-sorted staging stream (merge.cpp merge_stage_build): a
+//             stable radix sort of every slice's terms by (slice, column), then column << 8 |
+//             id and the term's offset in its slice.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
 #include <vector>
 
+#include "merge.h"
 #include "sell.h"
 #include "sm_internal.h"
 
@@ -207,6 +211,34 @@ __global__ __launch_bounds__(256) void bd_fill_kernel(int64_t n_slices, int64_t 
     }
 }
 
+// Merge staging (merge.cpp merge_stage_build): per merge slice b, its terms [z0, z1) keyed by
+// (b, column) -- a stable sort then orders each slice's terms by column, ties in term order.
+__global__ __launch_bounds__(256) void bd_mkey_kernel(int64_t nb, const int32_t *__restrict__ corner,
+                                                      const int32_t *__restrict__ col,
+                                                      unsigned long long *__restrict__ key, int32_t *__restrict__ idx) {
+    for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const int32_t z0 = corner[2 * b + 1], z1 = corner[2 * b + 3];
+        for (int32_t e = z0 + (int32_t)threadIdx.x; e < z1; e += (int32_t)blockDim.x) {
+            key[e] = ((unsigned long long)b << 24) | (unsigned)col[e];
+            idx[e] = e;
+        }
+    }
+}
+
+// w = column << 8 | id, z = the term's offset in its slice (its original order there).
+__global__ __launch_bounds__(256) void bd_mstage_kernel(int64_t n, const unsigned long long *__restrict__ skey,
+                                                        const int32_t *__restrict__ sidx,
+                                                        const int32_t *__restrict__ corner,
+                                                        const int32_t *__restrict__ col, const uint8_t *__restrict__ ids,
+                                                        uint32_t *__restrict__ w, uint16_t *__restrict__ z) {
+    GS_LOOP(i, n) {
+        const int32_t e = sidx[i];
+        const int64_t b = (int64_t)(skey[i] >> 24);
+        w[i] = ((uint32_t)col[e] << 8) | ids[e];
+        z[i] = (uint16_t)(e - corner[2 * b + 1]);
+    }
+}
+
 struct Tmp {
     std::vector<void *> p;
     template <class T>
@@ -368,6 +400,42 @@ int devbuild_codebook(const float *d_val, int64_t n, std::vector<float> &table, 
     BD_TRY(hipMemcpy(d_tb, tb.data(), (size_t)K * 4, hipMemcpyHostToDevice));
     BD_TRY(hipMemcpy(d_tid, tid.data(), (size_t)K, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(bd_ids_kernel, dim3(grid_of(n)), dim3(256), 0, s, n, d_val, d_tb, d_tid, K, d_ids);
+    BD_TRY(hipGetLastError());
+    BD_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+int devbuild_merge_stage(sm_matrix *m, hipStream_t s, hipError_t &err) {
+    err = hipSuccess;
+    Plan &p = m->plan;
+    const int64_t nnz = m->nnz;
+    if (nnz <= 0 || m->n_cols > (1 << 24) || !p.d_merge_corner) return 1;   // merge_stage_build declines
+    const int32_t *col = p.n_relabel > 0 ? p.d_rcol : m->d_col;
+    const int32_t *corner = reinterpret_cast<const int32_t *>(p.d_merge_corner);
+    Tmp t;
+    uint8_t *ids = nullptr;
+    BD_TRY(t.alloc(&ids, nnz));
+    std::vector<float> table;
+    const int rc = devbuild_codebook(m->d_val, nnz, table, ids, s, err);
+    if (rc != 0) return rc;   // > 255 distinct values: declined (as codebook_ids)
+    const int64_t nb = merge_blocks(m->n_rows, nnz);
+    unsigned long long *key = nullptr, *skey = nullptr;
+    int32_t *idx = nullptr, *sidx = nullptr;
+    BD_TRY(t.alloc(&key, nnz));
+    BD_TRY(t.alloc(&skey, nnz));
+    BD_TRY(t.alloc(&idx, nnz));
+    BD_TRY(t.alloc(&sidx, nnz));
+    hipLaunchKernelGGL(bd_mkey_kernel, dim3((unsigned)std::min<int64_t>(nb, 1 << 16)), dim3(256), 0, s, nb, corner, col,
+                       key, idx);
+    BD_TRY(hipGetLastError());
+    BD_TRY(sort_pairs(t, key, skey, idx, sidx, nnz, 24 + bits_for((uint32_t)std::max<int64_t>(nb - 1, 1)), s));
+    BD_TRY(keep_alloc(&p.d_mstage_w, nnz, m->device_bytes));
+    BD_TRY(keep_alloc(&p.d_mstage_z, nnz, m->device_bytes));
+    BD_TRY(keep_alloc(&p.d_mstage_tab, 256, m->device_bytes));
+    table.resize(256, 0.0f);
+    BD_TRY(hipMemcpy(p.d_mstage_tab, table.data(), 256 * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(bd_mstage_kernel, dim3(grid_of(nnz)), dim3(256), 0, s, nnz, skey, sidx, corner, col, ids,
+                       p.d_mstage_w, p.d_mstage_z);
     BD_TRY(hipGetLastError());
     BD_TRY(hipStreamSynchronize(s));
     return 0;

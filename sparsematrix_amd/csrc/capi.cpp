@@ -1494,13 +1494,12 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
     st = upload_plan(m.get(), rp.data());
     const bool xband = want_xband(m.get());
     // The column relabeling and the sorted sliced ELL on the device (builddev.hip) where they
-    // are all this matrix wants: no band layout, sweep, hot split, merge staging copy, windowed
-    // sort or exact sliced ELL, and no column-chunked ELL once the relabeling is decided (its
-    // builder runs on the host).  R-MAT 24: the host path took 5.4 s.
+    // are all this matrix wants: no band layout, sweep, hot split, windowed sort or exact sliced
+    // ELL, and no column-chunked ELL once the relabeling is decided (its builder runs on the
+    // host).  R-MAT 24: the host path took 5.4 s.
     bool dev_done = false;
     const bool dev_ok = st == SM_OK && m->opts.host_build == 0 && !want_sweep(m.get()) && m->opts.hot_cols <= 0 &&
-                        !want_merge_stage(m.get()) && m->opts.sell_sigma == 0 && m->opts.sell_streams <= 1 &&
-                        m->opts.exact_sell != 1;
+                        m->opts.sell_sigma == 0 && m->opts.sell_streams <= 1 && m->opts.exact_sell != 1;
     // The gathered chunk bands on the device (builddev_gcb.hip; config 5: 15 s on the host path).
     // Declined (a row's columns not ascending, size limits): the host path below decides.
     if (dev_ok && xband && xband_kind_setting(m.get()) == kXbGcb) {
@@ -1528,6 +1527,12 @@ sm_status sm_create_from_csr_device_ex(int64_t n_rows, int64_t n_cols, int64_t n
             dev_done = rc == 0;
         }
         if (rc != 0) st = hip_fail(eb, "device layout builder");
+    }
+    // The merge path's staging copy (sm_build_opts.merge_stage) after a device build too
+    // (R-MAT 24: 7.7 s on the host path).
+    if (st == SM_OK && dev_done && want_merge_stage(m.get())) {
+        hipError_t eb = hipSuccess;
+        if (devbuild_merge_stage(m.get(), s, eb) < 0) st = hip_fail(eb, "device merge staging builder");
     }
     const bool maybe_sell = m->opts.sell != 0 && nnz > 0;
     // The band / sell builders run on the host (band2.cpp, xband.cpp, sell.cpp): the
@@ -1658,7 +1663,6 @@ sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]) {
         Fnv w;
         if ((st = fnv_dev(w, xb.d_word, (int64_t)xb.n_bands * kGcbBandWords)) != SM_OK) return st;
         digest[2] = w.h;
-        return SM_OK;
     }
     const SellDev &d = p.sell;
     if (d.n_slices > 0) {
@@ -1681,13 +1685,21 @@ sm_status sm_layout_digest(const sm_matrix *m, uint64_t digest[4]) {
         if ((st = fnv_dev(c, d.d_col, padded + 32 * kSellLanes)) != SM_OK) return st;
         if ((st = fnv_dev(c, d.d_val, d.d_val ? padded + 32 * kSellLanes : 0)) != SM_OK) return st;
         digest[2] = c.h;
-        if (d.d_table) {
-            Fnv t;
-            if ((st = fnv_dev(t, d.d_table, d.table_size)) != SM_OK) return st;
-            t.add(&d.table_size, 4);
-            digest[3] = t.h;
-        }
     }
+    Fnv t;   // [3]: the sliced ELL's codebook, then the merge staging copy
+    bool any = false;
+    if (d.n_slices > 0 && d.d_table) {
+        if ((st = fnv_dev(t, d.d_table, d.table_size)) != SM_OK) return st;
+        t.add(&d.table_size, 4);
+        any = true;
+    }
+    if (p.d_mstage_w) {
+        if ((st = fnv_dev(t, p.d_mstage_w, m->nnz)) != SM_OK) return st;
+        if ((st = fnv_dev(t, p.d_mstage_z, m->nnz)) != SM_OK) return st;
+        if ((st = fnv_dev(t, p.d_mstage_tab, 256)) != SM_OK) return st;
+        any = true;
+    }
+    if (any) digest[3] = t.h;
     return SM_OK;
 }
 

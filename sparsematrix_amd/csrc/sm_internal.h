@@ -306,6 +306,9 @@ int encode_csr_ref_device(const int32_t *d_rp, const int32_t *d_col, const float
 // upload_sell build on the host.  0 built or declined as the host would, -5 HIP error (err).
 int devbuild_relabel(sm_matrix *m, bool check_skew, hipStream_t s, hipError_t &err);
 int devbuild_sell(sm_matrix *m, int32_t max_len, bool codebook, hipStream_t s, hipError_t &err);
+// The merge path's staging stream (merge_stage_build's bytes) from the device CSR and the
+// plan's slice corners: 0 built, 1 declined as the host would, < 0 on a HIP error (err).
+int devbuild_merge_stage(sm_matrix *m, hipStream_t s, hipError_t &err);
 // The gathered chunk bands (builddev_gcb.hip): gcb_build's bytes into m->plan.xb's d_chunk_start,
 // d_band_clo and d_word, the geometry in `meta` (its vectors stay empty).  0 built, 1 declined as
 // gcb_build would, < 0 on a HIP error (err) or a builder inconsistency.

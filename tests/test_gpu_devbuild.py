@@ -230,3 +230,36 @@ def test_devbuild_gcb_config5_rank0_slice(sm):
     H.spmv(x, yh, 1.0, 0.5)
     assert torch.equal(yd.view(torch.int32), yh.view(torch.int32))
     assert td < 1.5, (td, th)
+
+
+# ---- the merge path's staging copy (builddev.hip devbuild_merge_stage) ----------------------
+def test_devbuild_merge_stage_rmat_relabeled_and_plain(sm):
+    """sm_build_opts.merge_stage on a device CSR: R-MAT 18 (relabeled columns, codebook) and a
+    uniform matrix without relabeling -- the staging words, offsets and table byte-identical to
+    merge_stage_build's (digest [3]), SM_ALGO_MERGE the same bits either way."""
+    torch = torch_dev()
+    from gpu_util import uniform_csr
+    rp, ci, va = _rmat(18, 7)
+    cases = [(rp, ci, va, 1 << 18, 1 << 18, dict(layout="no_bands", relabel=1, merge_stage=1))]
+    r2, c2, v2 = uniform_csr(70000, 90000, 12, seed=4)
+    cases.append(tuple(torch.from_numpy(a).cuda() for a in (r2, c2, v2)) + (70000, 90000, dict(merge_stage=1)))
+    for rp_, ci_, va_, n_rows, n_cols, opts in cases:
+        D, H, info = _both(sm, rp_, ci_, va_, n_cols, opts)
+        assert info["merge_stage"] == 1 and D.layout_digest()[3] != 0, info
+        g = torch.Generator(device="cuda").manual_seed(9)
+        x = torch.rand(n_cols, device="cuda", generator=g) * 2 - 1
+        y0 = torch.rand(n_rows, device="cuda", generator=g) * 2 - 1
+        yd, yh = y0.clone(), y0.clone()
+        D.spmv(x, yd, 1.3, 0.5, algo="merge")
+        H.spmv(x, yh, 1.3, 0.5, algo="merge")
+        assert torch.equal(yd.view(torch.int32), yh.view(torch.int32))
+
+
+def test_devbuild_merge_stage_declines_beyond_codebook(sm):
+    """More than 255 distinct values: both builders decline the staging copy."""
+    torch = torch_dev()
+    rp, ci, _ = _rmat(14, 3)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    va = torch.rand(ci.numel(), device="cuda", generator=g)
+    D, H, info = _both(sm, rp, ci, va, 1 << 14, dict(layout="no_bands", merge_stage=1))
+    assert info["merge_stage"] == 0, info
