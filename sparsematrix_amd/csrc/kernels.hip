@@ -450,23 +450,28 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float *__restrict_
     }
 }
 
+// Device CSR ingestion: one grid-stride pass over max(rows + 1, terms) -- row i checks its
+// pointers, term i its column (a per-row loop over the terms took 12 ms on R-MAT 24, whose
+// longest row has 238 K terms).
 __global__ __launch_bounds__(256) void validate_kernel(int32_t n_rows, int32_t n_cols, int32_t nnz,
                                                        const int32_t *__restrict__ rp,
                                                        const int32_t *__restrict__ col,
                                                        int32_t *flag) {
-    const int32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > n_rows) return;
-    if (r == 0 && rp[0] != 0) atomicOr(flag, 1);
-    if (r == n_rows) {
-        if (rp[n_rows] != nnz) atomicOr(flag, 2);
-        return;
+    const int64_t n = max((int64_t)n_rows + 1, (int64_t)nnz);
+    int32_t f = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i == 0 && rp[0] != 0) f |= 1;
+        if (i == n_rows && rp[n_rows] != nnz) f |= 2;
+        if (i < n_rows) {
+            const int32_t a = rp[i], e = rp[i + 1];
+            if (a > e || a < 0 || e > nnz) f |= 4;
+        }
+        if (i < nnz) {
+            const int32_t c = col[i];
+            if (c < 0 || c >= n_cols) f |= 8;
+        }
     }
-    const int32_t a = rp[r], e = rp[r + 1];
-    if (a > e || a < 0 || e > nnz) { atomicOr(flag, 4); return; }
-    for (int32_t k = a; k < e; ++k) {
-        const int32_t c = col[k];
-        if (c < 0 || c >= n_cols) { atomicOr(flag, 8); return; }
-    }
+    if (f) atomicOr(flag, f);
 }
 
 __global__ __launch_bounds__(256) void scatter_dense_kernel(int32_t n, const int32_t *__restrict__ rp,
@@ -653,7 +658,8 @@ hipError_t launch_transpose(const float *a, int32_t m, int32_t n, int64_t lda, f
 
 hipError_t launch_validate(int32_t n_rows, int32_t n_cols, int32_t nnz, const int32_t *rp,
                            const int32_t *col, int32_t *d_flag, hipStream_t s) {
-    hipLaunchKernelGGL(validate_kernel, dim3(blocks_for((int64_t)n_rows + 1)), dim3(256), 0, s,
+    const int64_t n = std::max<int64_t>((int64_t)n_rows + 1, nnz);
+    hipLaunchKernelGGL(validate_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1 << 16)), dim3(256), 0, s,
                        n_rows, n_cols, nnz, rp, col, d_flag);
     return hipGetLastError();
 }

@@ -263,3 +263,36 @@ def test_devbuild_merge_stage_declines_beyond_codebook(sm):
     va = torch.rand(ci.numel(), device="cuda", generator=g)
     D, H, info = _both(sm, rp, ci, va, 1 << 14, dict(layout="no_bands", merge_stage=1))
     assert info["merge_stage"] == 0, info
+
+
+def test_device_csr_validation_flags(sm):
+    """sm_create_from_csr_device rejects what the host path rejects (validate_kernel: row
+    pointers start at 0, end at nnz, never decrease; columns in range) -- including a bad
+    column deep inside one long row -- and accepts the repaired arrays."""
+    torch = torch_dev()
+    rng = np.random.default_rng(4)
+    n_rows, n_cols = 5000, 3000
+    lens = rng.integers(0, 9, n_rows)
+    lens[1234] = 2500
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = np.concatenate([np.sort(rng.choice(n_cols, int(k), replace=False)) for k in lens]).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size).astype(np.float32)
+
+    def build(r, c):
+        dev = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (r, c, va)]
+        return sm.SparseMatrix.from_csr(*dev, n_cols)
+
+    build(rp, ci)   # valid
+    bad_col = ci.copy()
+    bad_col[rp[1234] + 2000] = n_cols
+    neg_col = ci.copy()
+    neg_col[-1] = -1
+    bad_first = rp.copy()
+    bad_first[0] = 1
+    bad_last = rp.copy()
+    bad_last[-1] -= 1
+    bad_order = rp.copy()
+    bad_order[100], bad_order[101] = bad_order[101] + 1, bad_order[100]
+    for r, c in ((rp, bad_col), (rp, neg_col), (bad_first, ci), (bad_last, ci), (bad_order, ci)):
+        with pytest.raises(sm.SparseMatrixError):
+            build(r, c)
